@@ -1,0 +1,267 @@
+#!/usr/bin/env python3
+"""Benchmark: feature-metric PnP refinements/s on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1] shape, batched as configs[2]): every GPU refines
+its own batch of B independent queries, each N=512 points, C=256 channels,
+240x320 hypercolumn (960x1280 image, stride 4), Geman-McClure, lambda0=0.01,
+50 LM iterations, fp32 texels / fp64 arithmetic.  Synthetic inputs (SURVEY.md
+§8d recipe; no dataset or CNN weights offline).  One step = one launch of the
+LM kernel over the whole batch (all 50 iterations of all B queries), with the
+packed features already resident in HBM.  Weak scaling: B queries per GPU;
+at 8 GPUs and B=128 this is configs[2] (1024 queries).  No collectives on the
+data path: ranks only meet in the timing barriers.
+
+Also reported: single-query latency (B=1, one query spread over several
+workgroups), the feature-pack kernel (fused Sobel + channels-last) rate, the
+roofline of the LM kernel, and the CPU baseline (the oracle's C restatement of
+the reference loop, OpenMP over queries) on a bounded sample.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+       N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "featuremetric-pnp_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+N_PTS, C, HF, WF, ITERS = 512, 256, 240, 320, 50
+HBM_PEAK = 8.0e12  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+B_ITER = N_PTS * (16 * C + 24)  # algorithmic bytes per GN iteration per query
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=128, help="queries per GPU")
+    ap.add_argument("--wgs", type=int, default=0, help="workgroups per query (0 = auto)")
+    ap.add_argument("--cpu-sample", type=int, default=512, help="queries in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-extras", action="store_true", help="skip single-query / pack / CPU legs")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import fmpnp
+    from fmpnp import _lib, refine as rf, synth
+
+    # ---------------- setup (untimed): this rank's queries, packed in HBM ----------------
+    B = args.batch
+    t0 = time.time()
+    probs = []
+    keep = []
+    for q in range(B):
+        seed = rank * 100003 + q
+        inp = synth.problem_inputs(N_PTS, C, HF, WF, seed=seed, device=dev)
+        feats = rf.pack_features(inp["fmap"], storage=torch.float32, device=dev)
+        probs.append(rf.make_problem(feats, inp["fref"], inp["pts3d"], inp["K"], inp["im_width"],
+                                     inp["im_height"], inp["R0"], inp["t0"]))
+        if q < 1:
+            keep.append(inp)
+        del inp
+    torch.cuda.synchronize()
+    if rank == 0:
+        log(f"[bench] setup {B} queries/GPU in {time.time() - t0:.1f}s "
+            f"({torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB resident)")
+    opts = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32, wgs_per_problem=args.wgs)
+    batch = rf.AsyncBatch(probs, opts)
+
+    # ---------------- warmup ----------------
+    for _ in range(args.warmup):
+        batch.launch()
+    torch.cuda.synchronize()
+    launch = _lib.last_launch()
+
+    # ---------------- timed region ----------------
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        batch.launch()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t_start
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    res = batch.results()
+    statuses = sorted({r["status"] for r in res})
+    if any(s & _lib.STATUS_SYNC_TIMEOUT for s in statuses):
+        raise RuntimeError("sync timeout in the LM kernel")
+
+    value = B * world * args.steps / elapsed
+    ms_step = 1e3 * elapsed / args.steps
+    avg_kernel_s = float(np.mean(kern_ms)) / 1e3
+    algo_bytes = B * ITERS * B_ITER
+    achieved = algo_bytes / avg_kernel_s
+
+    extras = {}
+    if rank == 0 and not args.no_extras:
+        extras = run_extras(args, dev, probs, keep, opts, rf, _lib, synth)
+
+    if rank == 0:
+        traffic = load_traffic(B)
+        out = {
+            "metric": "pose-refinements/sec (N=512 pts, C=256, 240x320, 50 LM iters)",
+            "value": round(value, 3),
+            "unit": "pose-refinements/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SURVEY.md §8d: smoothed L2-normalised random hypercolumns, seeded points)",
+            "config": {"workload": "configs[1] shape batched as configs[2]: B independent queries per GPU "
+                                   "(B=128 x 8 GPUs = 1024)",
+                       "points": N_PTS, "channels": C, "feature_map": f"{HF}x{WF}", "image": f"{4 * HF}x{4 * WF}",
+                       "iters": ITERS, "loss": "geman_mcclure", "lambda0": 0.01, "texel_storage": "f32",
+                       "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"query sharding x{world} (no collectives)",
+                       "launch": launch},
+            "gn_iters_per_s": round(value * ITERS, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
+                         "traffic": traffic,
+                         "kernel": "fmpnp::lm_kernel<float>", "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
+                         "algorithmic_bytes_per_launch": algo_bytes,
+                         "bytes_rule": "B * iters * N*(16C+24) (f, gx, gy, fref fp32 at one texel + fp64 point)"},
+            "statuses": statuses,
+        }
+        out.update(extras)
+        print(json.dumps(out), flush=True)
+    if dist:
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
+def load_traffic(B):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this workload, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("batch") == B:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def run_extras(args, dev, probs, keep, opts, rf, _lib, synth):
+    out = {}
+    # single-query latency: one query, workgroups of a team cooperate on its points
+    one = rf.AsyncBatch(probs[:1], opts)
+    for _ in range(3):
+        one.launch()
+    torch.cuda.synchronize()
+    reps = 20
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        one.launch()
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / reps
+    out["single_query"] = {"ms_per_refinement": round(ms, 4), "gn_iters_per_s": round(ITERS / (ms / 1e3), 1),
+                           "launch": _lib.last_launch()}
+    # feature pack kernel (fused Sobel + channels-last): 4C bytes read + 12C written per texel
+    fm = keep[0]["fmap"]
+    outbuf = torch.empty((HF, WF, 3, C), dtype=torch.float32, device=dev)
+    import ctypes
+    L = _lib.load()
+    st = _lib.stream_ptr(dev)
+
+    def pack():
+        rc = L.fmpnp_pack_features(ctypes.c_void_p(fm.data_ptr()), None, None, _lib.F32, C, HF, WF,
+                                   ctypes.c_void_p(outbuf.data_ptr()), _lib.F32, C, 0, 0, st)
+        _lib.check(rc, "pack")
+    for _ in range(3):
+        pack()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(20):
+        pack()
+    e.record()
+    torch.cuda.synchronize()
+    pms = s.elapsed_time(e) / 20
+    pbytes = 16 * C * HF * WF
+    out["pack"] = {"ms": round(pms, 4), "GB_per_s": round(pbytes / (pms / 1e3) / 1e9, 1),
+                   "frac_of_peak": round(pbytes / (pms / 1e3) / HBM_PEAK, 4)}
+    # CPU baseline: the oracle (C restatement of the reference loop), OpenMP over queries
+    if args.cpu_sample > 0 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        out["cpu_baseline"] = cpu_baseline(args, keep[0])
+    return out
+
+
+def cpu_baseline(args, inp0):
+    import oracle.oracle as orc
+    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    n_maps = min(threads, args.cpu_sample)
+    from fmpnp import synth
+    maps = []
+    for m in range(n_maps):
+        inp = synth.problem_inputs(N_PTS, C, HF, WF, seed=900000 + m, device="cpu")
+        fm = inp["fmap"].double().numpy()
+        gx, gy = orc.sobel(fm)
+        maps.append((inp, fm, gx, gy))
+    probs = []
+    for q in range(args.cpu_sample):
+        inp, fm, gx, gy = maps[q % n_maps]
+        probs.append(orc.make_problem(inp["pts3d"], inp["fref"].double().numpy(), fm, gx, gy, inp["K"],
+                                      inp["im_width"], inp["im_height"], inp["R0"], inp["t0"]))
+    opts = orc.make_options(ITERS, 0.01, "geman_mcclure")
+    orc.lib()
+    t = time.perf_counter()
+    orc.forward_batch(probs, opts, threads)
+    dt = time.perf_counter() - t
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(args.cpu_sample / dt, 4), "unit": "pose-refinements/s", "cores": threads,
+            "kind": "port", "gn_iters_per_s": round(args.cpu_sample * ITERS / dt, 1),
+            "sample": f"{args.cpu_sample} cfg2 queries ({n_maps} distinct maps), 50 iters each, fp64 CHW "
+                      f"reference layout, {dt:.1f}s", "cpu": cpu_model}
+
+
+if __name__ == "__main__":
+    main()

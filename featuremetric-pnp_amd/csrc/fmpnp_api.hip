@@ -1,0 +1,306 @@
+// fmpnp_api.hip -- the C ABI of libfmpnp.so (declared in include/fmpnp.h).
+//
+// Host-side launch planning for the LM kernel: how many workgroups cooperate on a
+// problem (G), how many problem teams are resident at once, the dynamic LDS carve
+// and the per-team exchange workspace.  No compute happens here; there is no CPU
+// fallback of any kernel.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+
+#include "fmpnp.h"
+#include "fmpnp_internal.h"
+
+using namespace fmpnp;
+
+namespace {
+
+struct Plan {
+    int G = 1, teams = 1, teams_pad = 8, gw = 8, grid = 8, nc_max = 1, max_n = 0;
+    int tex_bytes = 0, rec_bytes = 0, lds = 0;
+    bool vec = true;
+    size_t ws_counters = 0, ws_partials = 0, ws_max = 0, ws_total = 0;
+};
+
+thread_local Plan g_last;
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int elem_size(int dtype) { return dtype == FMPNP_F64 ? 8 : 4; }
+
+int validate(const fmpnp_problem *probs, int n, const fmpnp_options *opt) {
+    if (!opt || n < 0 || (n > 0 && !probs)) return FMPNP_EINVAL;
+    if (opt->dtype != FMPNP_F32 && opt->dtype != FMPNP_F64) return FMPNP_EINVAL;
+    if (opt->loss < FMPNP_SQUARED || opt->loss > FMPNP_BARRON) return FMPNP_EINVAL;
+    if (opt->mode != FMPNP_MODE_FORWARD && opt->mode != FMPNP_MODE_COMPUTE_COST) return FMPNP_EINVAL;
+    if (opt->sampling != FMPNP_NEAREST) return FMPNP_EINVAL;  // bilinear: not in this build
+    for (int i = 0; i < n; ++i) {
+        const fmpnp_problem &p = probs[i];
+        if (p.N < 0 || p.Hf <= 0 || p.Wf <= 0 || p.im_width <= 0 || p.im_height <= 0) return FMPNP_EINVAL;
+        if (p.c_begin < 0 || p.c_end < p.c_begin || p.c_end > p.cstride || p.c_end > p.ld_ref) return FMPNP_EINVAL;
+        if (p.N > 0 && (!p.feat || !p.fref || !p.pts3d)) return FMPNP_EINVAL;
+        // every projected pixel maps to a texel < Hf*Wf; the packed map must hold 3*cstride per texel
+        if ((long long)p.Hf * p.Wf * 3 * (long long)p.cstride > (1LL << 40)) return FMPNP_ETOOBIG;
+    }
+    return 0;
+}
+
+bool vec_ok(const fmpnp_problem &p, int dtype) {
+    const int V = dtype == FMPNP_F64 ? 2 : 4;
+    const int es = elem_size(dtype);
+    auto al = [&](const void *ptr) { return ((uintptr_t)ptr % 16) == 0; };
+    return al(p.feat) && al(p.fref) && p.cstride % V == 0 && p.ld_ref % V == 0 && p.c_begin % V == 0 &&
+           (p.c_end - p.c_begin) % V == 0 && es * V == 16;
+}
+
+int device_cus(int *ncu) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return (int)e;
+    e = hipDeviceGetAttribute(ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    return (int)e;
+}
+
+int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan *pl) {
+    int rc = validate(probs, n, opt);
+    if (rc) return rc;
+    Plan P;
+    P.max_n = 0;
+    P.vec = true;
+    for (int i = 0; i < n; ++i) {
+        P.max_n = std::max(P.max_n, probs[i].N);
+        if (probs[i].N > 0 && !vec_ok(probs[i], opt->dtype)) P.vec = false;
+    }
+    P.nc_max = std::max(1, (P.max_n + CH - 1) / CH);
+    int ncu = 256;
+    rc = device_cus(&ncu);
+    if (rc) return rc;
+    // workgroups per problem: enough workgroups in flight to cover the chip (about two per
+    // CU), never more than the chunks of the largest problem, and few enough points per
+    // workgroup that its records fit a 64 KiB LDS budget.
+    const int lds_budget = 64 * 1024;
+    auto lds_for = [&](int G) {
+        int m = ((P.nc_max + G - 1) / G) * CH;
+        int tex = (int)align_up((size_t)m * 4, 16);
+        int rec = m * RECW * 8;
+        int part = G == 1 ? P.nc_max * NV * 8 : 0;
+        return lds_fixed_bytes() + tex + rec + part;
+    };
+    int G;
+    if (opt->wgs_per_problem > 0) {
+        G = std::min(opt->wgs_per_problem, P.nc_max);
+    } else {
+        int target = 2 * ncu;
+        G = n > 0 ? (target + n - 1) / n : 1;
+        G = std::max(1, std::min(G, P.nc_max));
+    }
+    G = std::min(G, MAX_G);
+    while (G < std::min(P.nc_max, MAX_G) && lds_for(G) > lds_budget) ++G;
+    if (lds_for(G) > 160 * 1024) return FMPNP_ETOOBIG;
+    P.G = G;
+    int m = ((P.nc_max + G - 1) / G) * CH;
+    P.tex_bytes = (int)align_up((size_t)m * 4, 16);
+    P.rec_bytes = m * RECW * 8;
+    P.lds = lds_for(G);
+    // resident capacity: every workgroup of a team must be co-resident (teams spin on each
+    // other).  Occupancy API minus one block per CU of margin (it can over-report by one).
+    int per_cu = 1;
+    {
+        int nb = 0;
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lm_kernel_ptr(opt->dtype), NT, P.lds);
+        if (e != hipSuccess) return (int)e;
+        per_cu = nb > 1 ? nb - 1 : 1;
+        per_cu = std::min(per_cu, 4);
+    }
+    long cap = (long)ncu * per_cu;
+    if (G == 1) cap = std::max(cap, (long)n);  // no cross-workgroup waits: any grid is safe
+    long max_teams = cap / G;
+    if (opt->max_teams > 0) max_teams = std::min<long>(max_teams, opt->max_teams);
+    // teams are padded to a multiple of the mapping group (8, the XCD count, or fewer
+    // teams) for the XCD-aware blockIdx mapping; the padded grid stays within the
+    // resident capacity
+    long teams = std::min<long>(std::max(n, 1), max_teams);
+    auto padded = [](long t) { long gw = t >= 8 ? 8 : t; return ((t + gw - 1) / gw) * gw; };
+    while (teams > 1 && G > 1 && padded(teams) * G > cap) --teams;
+    if (teams < 1 || (G > 1 && padded(teams) * G > cap)) return FMPNP_ETOOBIG;
+    P.teams = (int)teams;
+    P.gw = teams >= 8 ? 8 : (int)teams;
+    P.teams_pad = (int)padded(teams);
+    P.grid = P.teams_pad * G;
+    P.ws_counters = align_up((size_t)P.teams_pad * 16 * sizeof(unsigned), 256);
+    P.ws_partials = align_up((size_t)P.teams * 2 * P.nc_max * NV * sizeof(double), 256);
+    P.ws_max = align_up((size_t)P.teams * 2 * G * sizeof(double), 256);
+    P.ws_total = P.ws_counters + P.ws_partials + P.ws_max;
+    *pl = P;
+    return 0;
+}
+
+struct SyncCache {
+    std::mutex mu;
+    int device = -1;
+    void *buf = nullptr;
+    size_t bytes = 0;
+};
+SyncCache g_cache;
+
+}  // namespace
+
+extern "C" {
+
+int fmpnp_abi_version(void) { return FMPNP_ABI_VERSION; }
+
+const char *fmpnp_build_info(void) {
+    return "fmpnp gfx950: lm_kernel(NT=256, CH=16, NV=32, fp64 accumulation), pack_kernel(Sobel+HWC3), "
+           "gather_ref_kernel";
+}
+
+int fmpnp_device_check(int device) {
+    hipDeviceProp_t prop;
+    hipError_t e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) return (int)e;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return FMPNP_ENODEV;
+    return 0;
+}
+
+int fmpnp_pack_features(const void *chw, const void *gx_chw, const void *gy_chw, int dtype_in, int C, int H, int W,
+                        void *out, int dtype_out, int cstride, int sobel_normalized, int sobel_replicate_pad,
+                        void *hip_stream) {
+    if (!chw || !out || C <= 0 || H <= 0 || W <= 0 || cstride < C) return FMPNP_EINVAL;
+    if ((gx_chw == nullptr) != (gy_chw == nullptr)) return FMPNP_EINVAL;
+    if ((dtype_in != FMPNP_F32 && dtype_in != FMPNP_F64) || (dtype_out != FMPNP_F32 && dtype_out != FMPNP_F64))
+        return FMPNP_EINVAL;
+    return (int)launch_pack(chw, gx_chw, gy_chw, dtype_in, C, H, W, out, dtype_out, cstride, sobel_normalized,
+                            sobel_replicate_pad, (hipStream_t)hip_stream);
+}
+
+int fmpnp_gather_reference(const void *ref_chw, int dtype_in, int C, int H_ref, int W_ref, const double *ref_inliers,
+                           int N, int img0, int img1, void *out, int dtype_out, int ld_out, void *hip_stream) {
+    if (N == 0) return 0;
+    if (!ref_chw || !ref_inliers || !out || C <= 0 || H_ref <= 0 || W_ref <= 0 || N < 0 || ld_out < C || img0 <= 0 ||
+        img1 <= 0)
+        return FMPNP_EINVAL;
+    hipStream_t s = (hipStream_t)hip_stream;
+    int *err = nullptr;
+    hipError_t e = hipMallocAsync((void **)&err, sizeof(int), s);
+    if (e != hipSuccess) return (int)e;
+    (void)hipMemsetAsync(err, 0, sizeof(int), s);
+    e = launch_gather_ref(ref_chw, dtype_in, C, H_ref, W_ref, ref_inliers, N, img0, img1, out, dtype_out, ld_out, err,
+                          s);
+    int herr = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&herr, err, sizeof(int), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFreeAsync(err, s);
+    if (e != hipSuccess) return (int)e;
+    return herr ? FMPNP_EINVAL : 0;  // an inlier outside the reference map (reference: IndexError)
+}
+
+size_t fmpnp_workspace_size(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt) {
+    Plan P;
+    if (make_plan(probs_host, n, opt, &P)) return 0;
+    return P.ws_total;
+}
+
+int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem *probs_host, int n, int max_N,
+                             const fmpnp_options *opt, fmpnp_result *results_dev, fmpnp_trace_entry *trace_dev,
+                             int trace_stride, void *workspace, size_t workspace_bytes, void *hip_stream) {
+    (void)max_N;
+    if (n == 0) return 0;
+    if (!probs_dev || !probs_host || !results_dev) return FMPNP_EINVAL;
+    Plan P;
+    int rc = make_plan(probs_host, n, opt, &P);
+    if (rc) return rc;
+    if (workspace_bytes < P.ws_total || (!workspace && P.ws_total)) return FMPNP_ENOMEM;
+    hipStream_t s = (hipStream_t)hip_stream;
+    LaunchArgs a;
+    a.probs = probs_dev;
+    a.n = n;
+    a.opt = *opt;
+    a.results = results_dev;
+    a.trace = trace_dev;
+    a.trace_stride = trace_dev ? trace_stride : 0;
+    a.G = P.G;
+    a.teams = P.teams;
+    a.nc_max = P.nc_max;
+    a.gw = P.gw;
+    unsigned char *ws = (unsigned char *)workspace;
+    a.counters = (unsigned *)ws;
+    a.partials = (double *)(ws + P.ws_counters);
+    a.maxslots = (double *)(ws + P.ws_counters + P.ws_partials);
+    a.tex_bytes = P.tex_bytes;
+    a.rec_bytes = P.rec_bytes;
+    hipError_t e = hipMemsetAsync(a.counters, 0, P.ws_counters, s);
+    if (e != hipSuccess) return (int)e;
+    e = launch_lm(a, opt->dtype, P.grid, (size_t)P.lds, s);
+    g_last = P;
+    return (int)e;
+}
+
+int fmpnp_refine_batch(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt, fmpnp_result *results,
+                       fmpnp_trace_entry *trace, int trace_stride, void *hip_stream) {
+    if (n == 0) return 0;
+    if (!probs_host || !results) return FMPNP_EINVAL;
+    Plan P;
+    int rc = make_plan(probs_host, n, opt, &P);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)hip_stream;
+    const size_t b_probs = align_up(sizeof(fmpnp_problem) * n, 256);
+    const size_t b_res = align_up(sizeof(fmpnp_result) * n, 256);
+    const size_t b_tr = trace ? align_up(sizeof(fmpnp_trace_entry) * (size_t)n * trace_stride, 256) : 0;
+    const size_t need = b_probs + b_res + b_tr + P.ws_total;
+    std::lock_guard<std::mutex> lock(g_cache.mu);
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return (int)e;
+    if (g_cache.buf && (g_cache.bytes < need || g_cache.device != dev)) {
+        int cur = dev;
+        (void)hipSetDevice(g_cache.device);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(g_cache.buf);
+        (void)hipSetDevice(cur);
+        g_cache.buf = nullptr;
+        g_cache.bytes = 0;
+    }
+    if (!g_cache.buf) {
+        size_t bytes = std::max(need, (size_t)1 << 20);
+        e = hipMalloc(&g_cache.buf, bytes);
+        if (e != hipSuccess) return FMPNP_ENOMEM;
+        g_cache.bytes = bytes;
+        g_cache.device = dev;
+    }
+    unsigned char *base = (unsigned char *)g_cache.buf;
+    fmpnp_problem *d_probs = (fmpnp_problem *)base;
+    fmpnp_result *d_res = (fmpnp_result *)(base + b_probs);
+    fmpnp_trace_entry *d_tr = trace ? (fmpnp_trace_entry *)(base + b_probs + b_res) : nullptr;
+    void *d_ws = base + b_probs + b_res + b_tr;
+    e = hipMemcpyAsync(d_probs, probs_host, sizeof(fmpnp_problem) * n, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return (int)e;
+    if (d_tr) {
+        e = hipMemsetAsync(d_tr, 0, b_tr, s);
+        if (e != hipSuccess) return (int)e;
+    }
+    rc = fmpnp_refine_batch_async(d_probs, probs_host, n, P.max_n, opt, d_res, d_tr, trace_stride, d_ws, P.ws_total,
+                                  hip_stream);
+    if (rc) return rc;
+    e = hipMemcpyAsync(results, d_res, sizeof(fmpnp_result) * n, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return (int)e;
+    if (trace) {
+        e = hipMemcpyAsync(trace, d_tr, sizeof(fmpnp_trace_entry) * (size_t)n * trace_stride, hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) return (int)e;
+    }
+    e = hipStreamSynchronize(s);
+    return (int)e;
+}
+
+int fmpnp_last_launch(int *teams, int *wgs_per_problem, int *grid, int *lds_bytes) {
+    if (teams) *teams = g_last.teams;
+    if (wgs_per_problem) *wgs_per_problem = g_last.G;
+    if (grid) *grid = g_last.grid;
+    if (lds_bytes) *lds_bytes = g_last.lds;
+    return 0;
+}
+
+}  // extern "C"

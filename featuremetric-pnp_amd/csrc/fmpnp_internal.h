@@ -1,0 +1,43 @@
+// fmpnp_internal.h -- launch-side definitions shared by the fmpnp HIP sources.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+#include "fmpnp.h"
+
+namespace fmpnp {
+
+constexpr int NT = 256;         // threads per workgroup (4 waves)
+constexpr int CH = 16;          // points per reduction chunk (fixed: results do not depend on G)
+constexpr int NV = 32;          // reduced vector: 21 H + 6 g + rho + kept + supported + 2 pad
+constexpr int NGRP = NT / 16;   // 16-lane gather groups per workgroup
+constexpr int RECW = 8;         // per-point record: 6 channel sums + rho + rho'
+constexpr int MAX_G = 64;       // workgroups per problem
+
+// Kernel arguments (by value).
+struct LaunchArgs {
+    const fmpnp_problem *probs;   // device descriptors
+    int n;
+    fmpnp_options opt;
+    fmpnp_result *results;        // device
+    fmpnp_trace_entry *trace;     // device or null
+    int trace_stride;
+    int G, teams, nc_max, gw;     // gw: teams per XCD-mapping group (8, or fewer teams)
+    unsigned *counters;           // [teams_pad][16], zeroed every launch
+    double *partials;             // [teams][2][nc_max][NV]
+    double *maxslots;             // [teams][2][G]
+    int tex_bytes, rec_bytes;     // dynamic LDS carve
+};
+
+// Fixed LDS head: LMState + sync flag + per-wave maxima (sized generously, 16-B aligned).
+__host__ __device__ constexpr int lds_fixed_bytes() { return 1536; }
+
+hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream);
+const void *lm_kernel_ptr(int dtype);
+
+hipError_t launch_pack(const void *chw, const void *gx, const void *gy, int dtype_in, int C, int H, int W, void *out,
+                       int dtype_out, int cstride, int normalized, int replicate, hipStream_t stream);
+hipError_t launch_gather_ref(const void *ref, int dtype_in, int C, int H, int W, const double *inl, int N, int img0,
+                             int img1, void *out, int dtype_out, int ld_out, int *err, hipStream_t stream);
+
+}  // namespace fmpnp

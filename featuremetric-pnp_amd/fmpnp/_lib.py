@@ -1,0 +1,128 @@
+"""ctypes binding of libfmpnp.so (include/fmpnp.h).
+
+The library is the only compute path of this package: if it is missing, or no
+gfx950 device is visible, every entry point raises -- there is no CPU fallback.
+torch is imported first so that the process has exactly one HIP runtime
+(libamdhip64.so.7 is shared by SONAME with torch's bundled copy).
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before libfmpnp)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libfmpnp.so")
+
+# enums / constants (include/fmpnp.h)
+SQUARED, HUBER, CAUCHY, GEMAN_MCCLURE, BARRON = 0, 1, 2, 3, 4
+NEAREST, BILINEAR = 0, 1
+F32, F64 = 0, 1
+MODE_FORWARD, MODE_COMPUTE_COST = 0, 1
+STATUS_OK, STATUS_NO_SUPPORT, STATUS_NAN, STATUS_NO_SUPPORT_TRIAL, STATUS_SYNC_TIMEOUT = 0, 1, 2, 4, 8
+ERRORS = {-1: "EINVAL", -2: "EALIGN", -3: "ENOMEM", -4: "ETOOBIG", -5: "ENODEV"}
+
+
+class Options(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int), ("n_iters", ctypes.c_int), ("lambda0", ctypes.c_double),
+                ("use_ratio", ctypes.c_int), ("ratio_threshold", ctypes.c_double), ("loss", ctypes.c_int),
+                ("barron_alpha", ctypes.c_double), ("sampling", ctypes.c_int), ("dtype", ctypes.c_int),
+                ("wgs_per_problem", ctypes.c_int), ("max_teams", ctypes.c_int)]
+
+
+class Problem(ctypes.Structure):
+    _fields_ = [("feat", ctypes.c_void_p), ("fref", ctypes.c_void_p), ("pts3d", ctypes.c_void_p),
+                ("Hf", ctypes.c_int), ("Wf", ctypes.c_int), ("cstride", ctypes.c_int), ("c_begin", ctypes.c_int),
+                ("c_end", ctypes.c_int), ("ld_ref", ctypes.c_int), ("N", ctypes.c_int),
+                ("im_width", ctypes.c_int), ("im_height", ctypes.c_int),
+                ("K", ctypes.c_double * 9), ("R0", ctypes.c_double * 9), ("t0", ctypes.c_double * 3)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("R", ctypes.c_double * 9), ("t", ctypes.c_double * 3), ("initial_cost", ctypes.c_double),
+                ("best_cost", ctypes.c_double), ("final_lambda", ctypes.c_double), ("final_lr", ctypes.c_double),
+                ("best_num_inliers", ctypes.c_int), ("n_evals", ctypes.c_int), ("n_steps", ctypes.c_int),
+                ("n_accepted", ctypes.c_int), ("status", ctypes.c_int), ("has_best", ctypes.c_int)]
+
+
+class TraceEntry(ctypes.Structure):
+    _fields_ = [("R", ctypes.c_double * 9), ("t", ctypes.c_double * 3), ("cost", ctypes.c_double),
+                ("lambda_after", ctypes.c_double), ("lr_after", ctypes.c_double), ("n_supported", ctypes.c_int),
+                ("n_kept", ctypes.c_int), ("accepted", ctypes.c_int)]
+
+
+EXPORTS = ["fmpnp_abi_version", "fmpnp_build_info", "fmpnp_device_check", "fmpnp_pack_features",
+           "fmpnp_gather_reference", "fmpnp_workspace_size", "fmpnp_refine_batch_async", "fmpnp_refine_batch",
+           "fmpnp_last_launch"]
+
+_LIB = None
+
+
+class FmpnpError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libfmpnp.so (no device needed to load it)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise FmpnpError(f"libfmpnp.so not built ({LIB_PATH}); run `python -c 'import __graft_entry__ as g; "
+                         f"g.build()'` or `make -C featuremetric-pnp_amd`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i, d = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+    L.fmpnp_abi_version.restype = i
+    L.fmpnp_build_info.restype = ctypes.c_char_p
+    L.fmpnp_device_check.argtypes = [i]
+    L.fmpnp_device_check.restype = i
+    L.fmpnp_pack_features.argtypes = [vp, vp, vp, i, i, i, i, vp, i, i, i, i, vp]
+    L.fmpnp_pack_features.restype = i
+    L.fmpnp_gather_reference.argtypes = [vp, i, i, i, i, vp, i, i, i, vp, i, i, vp]
+    L.fmpnp_gather_reference.restype = i
+    L.fmpnp_workspace_size.argtypes = [ctypes.POINTER(Problem), i, ctypes.POINTER(Options)]
+    L.fmpnp_workspace_size.restype = ctypes.c_size_t
+    L.fmpnp_refine_batch_async.argtypes = [vp, ctypes.POINTER(Problem), i, i, ctypes.POINTER(Options), vp, vp, i, vp,
+                                           ctypes.c_size_t, vp]
+    L.fmpnp_refine_batch_async.restype = i
+    L.fmpnp_refine_batch.argtypes = [ctypes.POINTER(Problem), i, ctypes.POINTER(Options), ctypes.POINTER(Result),
+                                     ctypes.POINTER(TraceEntry), i, vp]
+    L.fmpnp_refine_batch.restype = i
+    L.fmpnp_last_launch.argtypes = [ctypes.POINTER(i)] * 4
+    L.fmpnp_last_launch.restype = i
+    if L.fmpnp_abi_version() != 1:
+        raise FmpnpError("libfmpnp ABI mismatch")
+    _LIB = L
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        name = ERRORS.get(rc, f"hipError {rc}")
+        raise FmpnpError(f"{what} failed: {name}")
+
+
+_DEVICE_OK = {}
+
+
+def require_device(device):
+    """The HIP path needs a gfx950 device; anything else is a hard error."""
+    if not torch.cuda.is_available():
+        raise FmpnpError("fmpnp needs an AMD MI355X (gfx950) GPU; none is visible (no CPU fallback)")
+    idx = torch.device(device).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    if idx not in _DEVICE_OK:
+        rc = load().fmpnp_device_check(idx)
+        if rc != 0:
+            raise FmpnpError(f"device {idx} is not a gfx950 (fmpnp_device_check -> {rc})")
+        _DEVICE_OK[idx] = True
+    return idx
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def last_launch():
+    v = [ctypes.c_int() for _ in range(4)]
+    load().fmpnp_last_launch(*[ctypes.byref(x) for x in v])
+    return dict(teams=v[0].value, wgs_per_problem=v[1].value, grid=v[2].value, lds_bytes=v[3].value)

@@ -1,0 +1,29 @@
+"""Defaults that the reference binds through gin (featurePnP/model.gin,
+input_configs/*.gin: sparseFeaturePnP.*, optimize_feature_pnp.*).
+
+gin is not part of this build; `configure()` sets the same bindings in-process.
+"""
+from . import losses
+
+_MODEL = dict(n_iters=50, loss_fn=losses.squared_loss, lambda_=0.01, verbose=False, ratio_threshold=None,
+              useGPU=True)  # featurePnP/model.gin:1-5
+_ADAPTER = dict(image_shape=(1024, 1024), feature_pyramid=None)
+
+
+def configure(**kwargs):
+    """configure(n_iters=50, loss_fn=..., ratio_threshold=..., image_shape=..., feature_pyramid=...)."""
+    for k, v in kwargs.items():
+        if k in _ADAPTER:
+            _ADAPTER[k] = v
+        else:
+            if isinstance(v, str) and k == "loss_fn":
+                v = losses.BY_NAME[v]
+            _MODEL[k] = v
+
+
+def model_kwargs():
+    return dict(_MODEL)
+
+
+def adapter_kwargs():
+    return dict(_ADAPTER)

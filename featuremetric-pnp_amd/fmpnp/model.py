@@ -1,0 +1,196 @@
+"""sparseFeaturePnP -- drop-in for featurePnP/model.py:155-494 running on the MI355X.
+
+Same constructor, methods, arguments, return values and attributes as the
+reference class; the LM loop itself is one HIP launch (libfmpnp.so).  Inputs may
+be CPU or GPU tensors / numpy arrays; outputs are fp64 CPU tensors like the
+reference's (model.py:491-494).
+
+Feature storage precision: fp64 inputs are kept in fp64 on the device (results
+match the reference to ~1e-15), fp32 inputs in fp32 (the reference's fp64 cast of
+an fp32 hypercolumn is exact, so only the Sobel gradients are rounded).  Pass
+`storage=torch.float32` to force fp32 texels for speed.
+"""
+import math
+import warnings
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import _lib
+from . import losses as _losses
+from . import refine as _rf
+
+
+def _to_np(x, shape=None):
+    a = x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x)
+    a = a.astype(np.float64)
+    return a.reshape(shape) if shape is not None else a
+
+
+class sparseFeaturePnP(nn.Module):
+    """featurePnP/model.py:155-168 (ctor), :170-176 (track), :178-213 (multilevel),
+    :216-243 (compute_cost), :245-494 (forward)."""
+
+    def __init__(self, n_iters, loss_fn=_losses.squared_loss, lambda_=0.01, verbose=False, ratio_threshold=None,
+                 useGPU=False, storage=None, device=None, wgs_per_problem=0):
+        super().__init__()
+        self.iterations = n_iters
+        self.loss_fn = loss_fn
+        self.verbose = verbose
+        self.lambda_ = lambda_
+        self.track_ = {"Rs": [], "ts": [], "costs": [], "points2d": [], "mask": [], "threshold_mask": []}
+        self.use_ratio_test_ = ratio_threshold is not None
+        self.ratio_threshold_ = ratio_threshold
+        self.initial_cost_ = None
+        self.useGPU = useGPU  # accepted for compatibility: the refiner always runs on the GPU
+        self.storage = storage
+        self.device = device
+        self.wgs_per_problem = wgs_per_problem
+        self.status_ = None
+        self.last_result_ = None
+
+    # -- reference API --------------------------------------------------------
+    def track(self, R, t, cost, points_2d, mask, threshold_mask):
+        self.track_["Rs"].append(R)
+        self.track_["ts"].append(t)
+        self.track_["costs"].append(cost)
+        self.track_["points2d"].append(points_2d)
+        self.track_["mask"].append(mask)
+        self.track_["threshold_mask"].append(threshold_mask)
+
+    def _device(self, *tensors):
+        if self.device is not None:
+            return torch.device(self.device)
+        for t in tensors:
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                return t.device
+        return torch.device("cuda", torch.cuda.current_device())
+
+    def _options(self, storage_code, mode=_lib.MODE_FORWARD, loss=None):
+        code, alpha = _losses.resolve(self.loss_fn) if loss is None else (loss, 0.0)
+        return _rf.make_options(self.iterations, self.lambda_, code, alpha,
+                                self.ratio_threshold_ if self.use_ratio_test_ else None, storage_code, mode,
+                                self.wgs_per_problem)
+
+    def _storage_for(self, fmap):
+        if self.storage is not None:
+            return self.storage
+        dt = fmap.dtype if isinstance(fmap, torch.Tensor) else torch.as_tensor(np.asarray(fmap)).dtype
+        return torch.float64 if dt == torch.float64 else torch.float32
+
+    def forward(self, pts3D, feature_ref, feature_map_query, feature_grad_x, feature_grad_y, K, im_width, im_height,
+                R_init=None, t_init=None, track=False, confidence=None, scale=None):
+        """model.py:245-494.  Returns (R_best, t_best) as fp64 CPU tensors."""
+        dev = self._device(feature_map_query, pts3D)
+        storage = self._storage_for(feature_map_query)
+        feats = _rf.pack_features(feature_map_query, feature_grad_x, feature_grad_y, storage=storage, device=dev)
+        return self._forward_packed(feats, pts3D, feature_ref, K, im_width, im_height, R_init, t_init, track)
+
+    def _forward_packed(self, feats, pts3D, feature_ref, K, im_width, im_height, R_init=None, t_init=None,
+                        track=False, c_begin=0, c_end=None):
+        R0 = np.eye(3) if R_init is None else _to_np(R_init, (3, 3))          # model.py:271-273
+        t0 = np.array([1.0, 1.0, 0.0]) if t_init is None else _to_np(t_init, (3,))  # model.py:275-276
+        pts_np = _to_np(pts3D, (-1, 3))
+        # a channel-sliced level uses columns [c_begin, c_end) of the full-width fref
+        prob = _rf.make_problem(feats, feature_ref, pts3D if isinstance(pts3D, torch.Tensor) else pts_np, _to_np(K, (3, 3)),
+                                im_width, im_height, R0, t0, c_begin, c_end)
+        opts = self._options(feats.dtype_code)
+        want_trace = bool(track) or bool(self.verbose)
+        (res,), traces = _rf.refine([prob], opts, trace=want_trace)
+        self.last_result_ = res
+        self.status_ = res["status"]
+        if res["has_best"]:
+            self.best_cost_ = torch.tensor(res["best_cost"], dtype=torch.float64)
+            self.best_num_inliers_ = int(res["best_num_inliers"])
+            if self.initial_cost_ is None:
+                self.initial_cost_ = torch.tensor(res["initial_cost"], dtype=torch.float64)
+        if traces is not None:
+            tr = traces[0]
+            Kn = _to_np(K, (3, 3))
+            for k in range(len(tr["cost"])):
+                if self.verbose:
+                    print("Iter " if k == 0 else "new cost is ", tr["cost"][k])
+                if track:
+                    p2d = _rf.project_pixels(tr["R"][k], tr["t"][k], pts_np, Kn)
+                    mask = (p2d[:, 0] >= 0) & (p2d[:, 1] >= 0) & (p2d[:, 0] < im_width) & (p2d[:, 1] < im_height)
+                    self.track(torch.from_numpy(tr["R"][k].copy()), torch.from_numpy(tr["t"][k].copy()),
+                               float(tr["cost"][k]), torch.from_numpy(p2d), torch.from_numpy(mask), None)
+        if res["status"] & _lib.STATUS_NAN:
+            warnings.warn("NaN detected, exit (model.py:411-413)")
+        return (torch.from_numpy(res["R"].copy()), torch.from_numpy(res["t"].copy()))
+
+    def compute_cost(self, pts3D, R, t, feature_map_query, feature_ref, K, im_width, im_height):
+        """model.py:216-243: mean 0.5||e||^2 (no loss_fn, optional ratio test); None if no support."""
+        dev = self._device(feature_map_query, pts3D)
+        storage = self._storage_for(feature_map_query)
+        fm = feature_map_query if isinstance(feature_map_query, torch.Tensor) else torch.as_tensor(
+            np.asarray(feature_map_query))
+        z = torch.zeros_like(fm)
+        feats = _rf.pack_features(fm, z, z, storage=storage, device=dev)
+        return self._compute_cost_packed(feats, pts3D, R, t, feature_ref, K, im_width, im_height)
+
+    def _compute_cost_packed(self, feats, pts3D, R, t, feature_ref, K, im_width, im_height, c_begin=0, c_end=None):
+        prob = _rf.make_problem(feats, feature_ref, pts3D, _to_np(K, (3, 3)), im_width, im_height, _to_np(R, (3, 3)),
+                                _to_np(t, (3,)), c_begin, c_end)
+        opts = self._options(feats.dtype_code, _lib.MODE_COMPUTE_COST, loss=_lib.SQUARED)
+        (res,), _ = _rf.refine([prob], opts)
+        if res["status"] & _lib.STATUS_NO_SUPPORT:
+            return None
+        return torch.tensor(res["initial_cost"], dtype=torch.float64)
+
+    def multilevel_optimization(self, feature_pyramid, pts3D, feature_ref, feature_map_query, feature_grad_x,
+                                feature_grad_y, *args, **kwargs):
+        """model.py:178-213: coarse-to-fine over channel slices (optionally resized)."""
+        K, im_width, im_height = args[0], args[1], args[2]
+        R_init, t_init = kwargs.get("R_init"), kwargs.get("t_init")
+        track = kwargs.get("track", False)
+        dev = self._device(feature_map_query, pts3D)
+        storage = self._storage_for(feature_map_query)
+        fm = feature_map_query if isinstance(feature_map_query, torch.Tensor) else torch.as_tensor(
+            np.asarray(feature_map_query))
+        feats = _rf.pack_features(fm, feature_grad_x, feature_grad_y, storage=storage, device=dev)
+        return self._multilevel_packed(feature_pyramid, feats, fm, pts3D, feature_ref, K, im_width, im_height,
+                                       R_init, t_init, track)
+
+    def _multilevel_packed(self, feature_pyramid, feats, fm, pts3D, feature_ref, K, im_width, im_height, R_init,
+                           t_init, track):
+        self.initial_cost_ = self._compute_cost_packed(feats, pts3D, R_init, t_init, feature_ref, K, im_width,
+                                                       im_height)
+        if self.initial_cost_ is None:  # model.py:183-187
+            return R_init, t_init
+        if feature_pyramid is None:
+            return self._forward_packed(feats, pts3D, feature_ref, K, im_width, im_height, R_init, t_init, track)
+        R, t = R_init, t_init
+        C = feats.C
+        fref_t = feature_ref if isinstance(feature_ref, torch.Tensor) else torch.as_tensor(np.asarray(feature_ref))
+        for start, end, target_size, kernel_size in feature_pyramid:
+            end_c = min(end, C)  # python slicing clamps (model.py:194)
+            if target_size is None and kernel_size is None:
+                R, t = self._forward_packed(feats, pts3D, fref_t, K, im_width, im_height, R, t, track,
+                                            c_begin=start, c_end=end_c)
+                continue
+            # resized / blurred level (model.py:196-207): device resize, optional Gaussian, device Sobel
+            lvl = fm[start:end_c].to(self._device(fm), dtype=feats.dtype)[None]
+            if target_size is not None:
+                lvl = nn.functional.interpolate(lvl, size=(target_size, target_size), mode="bilinear")
+            if kernel_size is not None:
+                lvl = _gaussian_blur(lvl, kernel_size)
+            lf = _rf.pack_features(lvl[0], storage=feats.dtype, device=feats.buf.device)
+            R, t = self._forward_packed(lf, pts3D, fref_t[:, start:end_c], K, im_width, im_height, R, t, track)
+        return R, t
+
+
+def _gaussian_blur(x, kernel_size, sigma=1.0):
+    """kornia.filters.get_gaussian_kernel2d((k,k),(1,1)) + grouped conv2d padding=1 (model.py:199-200).
+    Parity unpinned: kornia 0.2.2 is not available to check against."""
+    k = kernel_size
+    xs = torch.arange(k, dtype=x.dtype, device=x.device) - (k - 1) / 2.0
+    g = torch.exp(-(xs ** 2) / (2.0 * sigma ** 2))
+    g = g / g.sum()
+    ker = torch.outer(g, g)[None, None].repeat(x.shape[1], 1, 1, 1)
+    return nn.functional.conv2d(x, ker, groups=x.shape[1], padding=1)
+
+
+def is_nan(x):
+    return x is None or (isinstance(x, float) and math.isnan(x))

@@ -1,0 +1,90 @@
+"""Adapter: feature_pnp / optimize_feature_pnp (s2dhm/pose_prediction/optimize_feature_pnp.py:50-91)
+and the DirectPoseModel call surface named by the build's north star.
+
+The reference copies the GPU hypercolumn to host fp64, gathers the reference
+descriptors with a per-point python loop, runs the Sobel on the CPU and then the
+LM loop on the CPU (optimize_feature_pnp.py:51-69).  Here the query hypercolumn
+stays on the device: one fused Sobel + channels-last pack kernel, one gather
+kernel for the reference descriptors, one LM launch.
+"""
+import numpy as np
+import torch
+
+from . import config
+from . import refine as _rf
+from .matrix_utils import matrix_quaternion
+from .model import sparseFeaturePnP
+
+
+def _new_model(model):
+    if model is not None:
+        return model
+    return sparseFeaturePnP(**config.model_kwargs())  # "Parameters from gin!" (optimize_feature_pnp.py:63)
+
+
+def feature_pnp(query_hypercolumns, reference_hypercolumns, prediction, K, image_shape, track=False,
+                feature_pyramid=None, model=None, storage=None):
+    """optimize_feature_pnp.py:50-71.  Returns (R, t, model) with R, t fp64 CPU tensors."""
+    model = _new_model(model)
+    q = query_hypercolumns[0] if query_hypercolumns.dim() == 4 else query_hypercolumns
+    dev = q.device if q.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    storage = storage or model.storage or (torch.float64 if q.dtype == torch.float64 else torch.float32)
+    feats = _rf.pack_features(q, storage=storage, device=dev)                               # :57, :61
+    fref = _rf.gather_reference(reference_hypercolumns, prediction.reference_inliers, image_shape,
+                                cstride=feats.cstride, storage=storage, device=dev)          # :51-56
+    pts3D = np.asarray(prediction.points_3d, dtype=np.float64).reshape(-1, 3)               # :52
+    T = np.asarray(prediction.matrix, dtype=np.float64)
+    R, t = torch.from_numpy(T[:3, :3].copy()), torch.from_numpy(T[:3, 3].copy())             # :59-60
+    Kt = K if isinstance(K, torch.Tensor) else torch.from_numpy(np.asarray(K, dtype=np.float64))
+    if feature_pyramid is None:                                                             # :64-69
+        R, t = model._forward_packed(feats, pts3D, fref, Kt, image_shape[0], image_shape[1], R, t, track)
+    else:
+        R, t = model._multilevel_packed(feature_pyramid, feats, q, pts3D, fref, Kt, image_shape[0], image_shape[1],
+                                        R, t, track)
+    return R, t, model
+
+
+def optimize_feature_pnp(query_hypercolumns, net, prediction, K, image_shape=None, track=False, feature_pyramid=None,
+                         features="s2dhm", model=None, verbose=False):
+    """optimize_feature_pnp.py:73-91.  Returns (list t, list quaternion, model)."""
+    cfg = config.adapter_kwargs()
+    image_shape = image_shape if image_shape is not None else cfg.get("image_shape", (1024, 1024))
+    if feature_pyramid is None:
+        feature_pyramid = cfg.get("feature_pyramid")
+    K = torch.from_numpy(np.asarray(K, dtype=np.float64))
+    if verbose:
+        print("Initial : {}".format(list(prediction.quaternion) + list(prediction.matrix[:3, 3])))
+    if features == "d2-net":
+        raise NotImplementedError("d2-net dense features are outside the refiner's scope")
+    reference_hypercolumns, _ = net.compute_hypercolumn([prediction.reference_filename], to_cpu=False, resize=True)
+    R, t, model = feature_pnp(query_hypercolumns, reference_hypercolumns, prediction, K, image_shape, track=track,
+                              feature_pyramid=feature_pyramid, model=model)
+    T = np.eye(4)
+    T[:3, :3], T[3, :3] = R.numpy(), t.numpy()  # the reference writes t into the bottom row (:87)
+    quaternion = matrix_quaternion(T)
+    if verbose:
+        print("Final : {}".format(list(quaternion) + list(t.numpy())))
+    return list(t.numpy()), list(quaternion), model
+
+
+class DirectPoseModel:
+    """The call surface named by the build's north star: `.optimize_feature_pnp()` with the
+    reference adapter's arguments, backed by the HIP refiner."""
+
+    def __init__(self, **model_kwargs):
+        self.model_kwargs = model_kwargs
+
+    def make_model(self):
+        kw = dict(config.model_kwargs())
+        kw.update(self.model_kwargs)
+        return sparseFeaturePnP(**kw)
+
+    def feature_pnp(self, query_hypercolumns, reference_hypercolumns, prediction, K, image_shape, track=False,
+                    feature_pyramid=None):
+        return feature_pnp(query_hypercolumns, reference_hypercolumns, prediction, K, image_shape, track,
+                           feature_pyramid, model=self.make_model())
+
+    def optimize_feature_pnp(self, query_hypercolumns, net, prediction, K, image_shape=None, track=False,
+                             feature_pyramid=None, features="s2dhm"):
+        return optimize_feature_pnp(query_hypercolumns, net, prediction, K, image_shape, track, feature_pyramid,
+                                    features, model=self.make_model())

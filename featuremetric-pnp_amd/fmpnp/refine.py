@@ -1,0 +1,306 @@
+"""Host-side plumbing of the HIP refiner: feature packing, problem descriptors,
+synchronous and asynchronous batched refinement.
+
+Everything here moves pointers and sizes into the C ABI of libfmpnp.so
+(include/fmpnp.h); torch provides device memory and streams only.
+"""
+import ctypes
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_TORCH2CODE = {torch.float32: _lib.F32, torch.float64: _lib.F64}
+_CODE2TORCH = {v: k for k, v in _TORCH2CODE.items()}
+
+
+def _dtype_code(dt):
+    if dt not in _TORCH2CODE:
+        raise TypeError(f"feature dtype must be float32 or float64, got {dt}")
+    return _TORCH2CODE[dt]
+
+
+def _round4(c):
+    return (c + 3) // 4 * 4
+
+
+@dataclass
+class PackedFeatures:
+    """Channels-last feature texels on the device: buf[H][W][3][cstride] = (f, gx, gy)."""
+    buf: torch.Tensor
+    C: int
+    H: int
+    W: int
+    cstride: int
+
+    @property
+    def dtype(self):
+        return self.buf.dtype
+
+    @property
+    def dtype_code(self):
+        return _dtype_code(self.buf.dtype)
+
+
+def _as_device(x, device, dtype=None):
+    t = x if isinstance(x, torch.Tensor) else torch.as_tensor(np.asarray(x))
+    t = t.to(device=device, dtype=dtype if dtype is not None else t.dtype)
+    return t.contiguous()
+
+
+def pack_features(fmap, gx=None, gy=None, storage=None, device=None, sobel_normalized=False,
+                  sobel_replicate_pad=False, stream=None):
+    """[C,H,W] (or [1,C,H,W]) feature map -> PackedFeatures.
+
+    Without gx/gy the Sobel gradients are computed on the device (fused kernel;
+    vendored kornia Sobel by default: unnormalised, zero padded,
+    featurePnP/helpers/sobel_pytorch.py).  With gx/gy they are packed as given
+    (sparseFeaturePnP.forward receives them from its caller).
+    """
+    fmap = fmap if isinstance(fmap, torch.Tensor) else torch.as_tensor(np.asarray(fmap))
+    if fmap.dim() == 4:
+        fmap = fmap[0]
+    if fmap.dim() != 3:
+        raise ValueError("feature map must be [C,H,W] or [1,C,H,W]")
+    device = torch.device(device) if device is not None else (
+        fmap.device if fmap.is_cuda else torch.device("cuda", torch.cuda.current_device()))
+    _lib.require_device(device)
+    in_dt = fmap.dtype if fmap.dtype in _TORCH2CODE else torch.float32
+    storage = storage or in_dt
+    C, H, W = fmap.shape
+    cs = _round4(C)
+    with torch.cuda.device(device):
+        f = _as_device(fmap, device, in_dt)
+        gxd = gyd = None
+        if gx is not None:
+            gxd = _as_device(gx.reshape(C, H, W) if isinstance(gx, torch.Tensor) else np.asarray(gx).reshape(C, H, W),
+                             device, in_dt)
+            gyd = _as_device(gy.reshape(C, H, W) if isinstance(gy, torch.Tensor) else np.asarray(gy).reshape(C, H, W),
+                             device, in_dt)
+        out = torch.zeros((H, W, 3, cs), dtype=storage, device=device) if cs != C else \
+            torch.empty((H, W, 3, cs), dtype=storage, device=device)
+        s = stream if stream is not None else _lib.stream_ptr(device)
+        rc = _lib.load().fmpnp_pack_features(
+            ctypes.c_void_p(f.data_ptr()), ctypes.c_void_p(gxd.data_ptr()) if gxd is not None else None,
+            ctypes.c_void_p(gyd.data_ptr()) if gyd is not None else None, _dtype_code(in_dt), C, H, W,
+            ctypes.c_void_p(out.data_ptr()), _dtype_code(storage), cs, int(bool(sobel_normalized)),
+            int(bool(sobel_replicate_pad)), s)
+        _lib.check(rc, "fmpnp_pack_features")
+        # keep inputs alive until the kernel has consumed them
+        if f.data_ptr() != fmap.data_ptr() or gxd is not None:
+            torch.cuda.current_stream(device).synchronize()
+    return PackedFeatures(out, C, H, W, cs)
+
+
+def pad_reference(fref, cstride, storage, device):
+    """fref [N,C] -> device [N, cstride] of the storage dtype (zero padded)."""
+    fref = fref if isinstance(fref, torch.Tensor) else torch.as_tensor(np.asarray(fref))
+    N, C = fref.shape
+    out = torch.zeros((N, cstride), dtype=storage, device=device)
+    out[:, :C] = fref.to(device=device, dtype=storage)
+    return out
+
+
+def gather_reference(ref_hc, reference_inliers, image_shape, cstride=None, storage=torch.float32, device=None):
+    """Device fref gather of optimize_feature_pnp.py:51-56 -> [N, cstride]."""
+    if ref_hc.dim() == 4:
+        ref_hc = ref_hc[0]
+    C, Hr, Wr = ref_hc.shape
+    device = torch.device(device) if device is not None else (
+        ref_hc.device if ref_hc.is_cuda else torch.device("cuda", torch.cuda.current_device()))
+    _lib.require_device(device)
+    in_dt = ref_hc.dtype if ref_hc.dtype in _TORCH2CODE else torch.float32
+    cs = cstride or _round4(C)
+    with torch.cuda.device(device):
+        ref = _as_device(ref_hc, device, in_dt)
+        inl = _as_device(torch.as_tensor(np.asarray(reference_inliers, dtype=np.float64).reshape(-1, 2)), device,
+                         torch.float64)
+        N = inl.shape[0]
+        out = torch.zeros((N, cs), dtype=storage, device=device)
+        rc = _lib.load().fmpnp_gather_reference(
+            ctypes.c_void_p(ref.data_ptr()), _dtype_code(in_dt), C, Hr, Wr, ctypes.c_void_p(inl.data_ptr()), N,
+            int(image_shape[0]), int(image_shape[1]), ctypes.c_void_p(out.data_ptr()), _dtype_code(storage), cs,
+            _lib.stream_ptr(device))
+        if rc == -1:
+            raise IndexError("a reference inlier maps outside the reference hypercolumn "
+                             "(optimize_feature_pnp.py:56 raises IndexError)")
+        _lib.check(rc, "fmpnp_gather_reference")
+    return out
+
+
+def _mat(x, shape):
+    a = np.asarray(x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else x, dtype=np.float64)
+    return a.reshape(shape)
+
+
+@dataclass
+class Problem:
+    """One refinement problem: packed query features + reference descriptors + points + pose."""
+    feats: PackedFeatures
+    fref: torch.Tensor          # device [N, ld] of feats.dtype
+    pts3d: torch.Tensor         # device [N, 3] float64
+    K: np.ndarray
+    im_width: int
+    im_height: int
+    R0: np.ndarray
+    t0: np.ndarray
+    c_begin: int = 0
+    c_end: int = None
+
+    def descriptor(self):
+        p = _lib.Problem()
+        f = self.feats
+        if self.fref.dtype != f.dtype:
+            raise TypeError("fref and packed features must share a dtype")
+        p.feat = f.buf.data_ptr()
+        p.fref = self.fref.data_ptr()
+        p.pts3d = self.pts3d.data_ptr()
+        p.Hf, p.Wf, p.cstride = f.H, f.W, f.cstride
+        p.c_begin = int(self.c_begin)
+        p.c_end = int(f.C if self.c_end is None else min(self.c_end, f.C))
+        p.ld_ref = self.fref.shape[1]
+        p.N = self.pts3d.shape[0]
+        p.im_width, p.im_height = int(self.im_width), int(self.im_height)
+        p.K[:] = list(_mat(self.K, 9))
+        p.R0[:] = list(_mat(self.R0, 9))
+        p.t0[:] = list(_mat(self.t0, 3))
+        return p
+
+
+def make_problem(feats, fref, pts3d, K, im_width, im_height, R0, t0, c_begin=0, c_end=None):
+    dev = feats.buf.device
+    pts = _as_device(torch.as_tensor(np.asarray(pts3d.detach().cpu() if isinstance(pts3d, torch.Tensor) else pts3d,
+                                                dtype=np.float64)).reshape(-1, 3), dev, torch.float64) \
+        if not (isinstance(pts3d, torch.Tensor) and pts3d.is_cuda and pts3d.dtype == torch.float64) \
+        else pts3d.reshape(-1, 3).contiguous()
+    if not (isinstance(fref, torch.Tensor) and fref.is_cuda and fref.dtype == feats.dtype
+            and fref.shape[1] % 4 == 0):
+        fref = pad_reference(fref, _round4(max(fref.shape[1], 1)), feats.dtype, dev)
+    return Problem(feats, fref.contiguous(), pts, K, im_width, im_height, R0, t0, c_begin, c_end)
+
+
+def make_options(n_iters, lambda0=0.01, loss=_lib.SQUARED, barron_alpha=0.0, ratio_threshold=None,
+                 dtype=_lib.F32, mode=_lib.MODE_FORWARD, wgs_per_problem=0, max_teams=0):
+    o = _lib.Options()
+    o.mode = int(mode)
+    o.n_iters = int(n_iters)
+    o.lambda0 = float(lambda0)
+    o.use_ratio = 0 if ratio_threshold is None else 1
+    o.ratio_threshold = 0.0 if ratio_threshold is None else float(ratio_threshold)
+    o.loss = int(loss)
+    o.barron_alpha = float(barron_alpha)
+    o.sampling = _lib.NEAREST
+    o.dtype = int(dtype)
+    o.wgs_per_problem = int(wgs_per_problem)
+    o.max_teams = int(max_teams)
+    return o
+
+
+def _result_dict(r):
+    return dict(R=np.array(r.R[:]).reshape(3, 3), t=np.array(r.t[:]), initial_cost=r.initial_cost,
+                best_cost=r.best_cost, final_lambda=r.final_lambda, final_lr=r.final_lr,
+                best_num_inliers=r.best_num_inliers, n_evals=r.n_evals, n_steps=r.n_steps,
+                n_accepted=r.n_accepted, status=r.status, has_best=bool(r.has_best))
+
+
+def _trace_dict(entries, n):
+    n = min(n, len(entries))
+    return dict(R=np.array([entries[i].R[:] for i in range(n)]).reshape(-1, 3, 3),
+                t=np.array([entries[i].t[:] for i in range(n)]).reshape(-1, 3),
+                cost=np.array([entries[i].cost for i in range(n)]),
+                lam=np.array([entries[i].lambda_after for i in range(n)]),
+                lr=np.array([entries[i].lr_after for i in range(n)]),
+                n_supported=np.array([entries[i].n_supported for i in range(n)]),
+                n_kept=np.array([entries[i].n_kept for i in range(n)]),
+                accepted=np.array([entries[i].accepted for i in range(n)], dtype=bool))
+
+
+def refine(problems, options, trace=False):
+    """Synchronous batched refinement.  Returns ([result dict], [trace dict] | None)."""
+    n = len(problems)
+    if n == 0:
+        return [], ([] if trace else None)
+    dev = problems[0].feats.buf.device
+    _lib.require_device(dev)
+    descs = (_lib.Problem * n)(*[p.descriptor() for p in problems])
+    if descs[0].feat and options.dtype != problems[0].feats.dtype_code:
+        raise TypeError("options.dtype does not match the packed features")
+    res = (_lib.Result * n)()
+    stride = max(1, options.n_iters + 1) if trace else 0
+    tr = (_lib.TraceEntry * (n * stride))() if trace else None
+    with torch.cuda.device(dev):
+        rc = _lib.load().fmpnp_refine_batch(descs, n, ctypes.byref(options), res, tr, stride, _lib.stream_ptr(dev))
+    _lib.check(rc, "fmpnp_refine_batch")
+    results = [_result_dict(r) for r in res]
+    traces = None
+    if trace:
+        traces = [_trace_dict(tr[i * stride:(i + 1) * stride], results[i]["n_evals"]) for i in range(n)]
+    for r in results:
+        if r["status"] & _lib.STATUS_SYNC_TIMEOUT:
+            raise _lib.FmpnpError("cross-workgroup exchange timed out (device oversubscribed?)")
+    return results, traces
+
+
+class AsyncBatch:
+    """Device-resident descriptors/results/workspace for repeated asynchronous launches
+    (the bench's timed region: nothing but the LM kernel and its counter memset)."""
+
+    def __init__(self, problems, options):
+        self.problems = list(problems)
+        self.options = options
+        n = len(self.problems)
+        self.n = n
+        self.dev = self.problems[0].feats.buf.device
+        _lib.require_device(self.dev)
+        self.descs_host = (_lib.Problem * n)(*[p.descriptor() for p in self.problems])
+        nbytes = ctypes.sizeof(_lib.Problem) * n
+        self.d_descs = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+        host = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(self.descs_host), nbytes)),
+                                dtype=torch.uint8)
+        self.d_descs.copy_(host)
+        self.d_res = torch.zeros(ctypes.sizeof(_lib.Result) * n, dtype=torch.uint8, device=self.dev)
+        ws = _lib.load().fmpnp_workspace_size(self.descs_host, n, ctypes.byref(options))
+        if ws == 0:
+            raise _lib.FmpnpError("fmpnp_workspace_size failed (invalid problems/options)")
+        self.d_ws = torch.empty(ws, dtype=torch.uint8, device=self.dev)
+        self.ws_bytes = ws
+        self.max_n = max(p.pts3d.shape[0] for p in self.problems)
+
+    def launch(self, stream=None):
+        s = stream if stream is not None else _lib.stream_ptr(self.dev)
+        rc = _lib.load().fmpnp_refine_batch_async(
+            ctypes.c_void_p(self.d_descs.data_ptr()), self.descs_host, self.n, self.max_n, ctypes.byref(self.options),
+            ctypes.c_void_p(self.d_res.data_ptr()), None, 0, ctypes.c_void_p(self.d_ws.data_ptr()),
+            self.ws_bytes, s)
+        _lib.check(rc, "fmpnp_refine_batch_async")
+
+    def results(self):
+        torch.cuda.current_stream(self.dev).synchronize()
+        raw = bytes(self.d_res.cpu().numpy().tobytes())
+        arr = (_lib.Result * self.n).from_buffer_copy(raw)
+        return [_result_dict(r) for r in arr]
+
+
+def project_pixels(R, t, pts3d, K):
+    """Host restatement of the pixel projection (model.py:303-308) for track_['points2d'];
+    elementwise numpy (no FMA), matching the device's sequential fp64 arithmetic."""
+    R = np.asarray(R, dtype=np.float64)
+    t = np.asarray(t, dtype=np.float64)
+    K = np.asarray(K, dtype=np.float64)
+    X = np.asarray(pts3d, dtype=np.float64).reshape(-1, 3)
+    P = [((R[i, 0] * X[:, 0] + R[i, 1] * X[:, 1]) + R[i, 2] * X[:, 2]) + t[i] for i in range(3)]
+    u = [((K[i, 0] * P[0] + K[i, 1] * P[1]) + K[i, 2] * P[2]) for i in range(3)]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        px = np.rint(u[0] / u[2]) - 1.0
+        py = np.rint(u[1] / u[2]) - 1.0
+    bad = ~np.isfinite(px) | ~np.isfinite(py) | (np.abs(px) > 2 ** 31 - 2) | (np.abs(py) > 2 ** 31 - 2)
+    px = np.where(bad, -(2 ** 31), px)
+    py = np.where(bad, -(2 ** 31), py)
+    return np.stack([px, py], 1).astype(np.int32)
+
+
+def nan_to_none(x):
+    return None if (x is None or (isinstance(x, float) and math.isnan(x))) else x

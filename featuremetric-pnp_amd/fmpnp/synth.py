@@ -1,0 +1,62 @@
+"""Synthetic refinement problems (SURVEY.md §8d recipe) for benches and tests.
+
+There is no dataset or CNN checkpoint offline, so the hypercolumn is a smoothed,
+L2-normalised random field of the reference's shape and dtype (fp32,
+L2-normalised over channels like network.py:172-173).  Image size = 4x the
+feature map (stride 4), K = [[0.8 W, 0, W/2], [0, 0.8 W, H/2], [0, 0, 1]],
+points uniformly inside the central 80 % of the image at depth U(5, 25),
+reference descriptors = the nearest-texel gather at the identity pose, initial
+pose Rz(1 deg), t = (0.05, -0.03, 0.10).
+"""
+import math
+
+import numpy as np
+import torch
+
+from .refine import project_pixels
+
+
+def rot_z(deg):
+    a = math.radians(deg)
+    return np.array([[math.cos(a), -math.sin(a), 0.0], [math.sin(a), math.cos(a), 0.0], [0.0, 0.0, 1.0]])
+
+
+def feature_map(C, Hf, Wf, seed, device):
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed))
+    x = torch.randn((1, C, Hf, Wf), generator=g, device=device, dtype=torch.float32)
+    x = torch.nn.functional.avg_pool2d(x, 7, stride=1, padding=3)
+    x = x / x.norm(dim=1, keepdim=True).clamp_min(1e-12)
+    return x[0].contiguous()
+
+
+def scene(N, Hf, Wf, seed):
+    rng = np.random.Generator(np.random.PCG64(int(seed) + 1000003))
+    W, H = 4 * Wf, 4 * Hf
+    K = np.array([[0.8 * W, 0.0, W / 2.0], [0.0, 0.8 * W, H / 2.0], [0.0, 0.0, 1.0]])
+    u = rng.uniform(0.1, 0.9, N) * W
+    v = rng.uniform(0.1, 0.9, N) * H
+    z = rng.uniform(5.0, 25.0, N)
+    X = np.stack([(u - K[0, 2]) * z / K[0, 0], (v - K[1, 2]) * z / K[1, 1], z], 1)
+    return X, K, W, H
+
+
+def reference_descriptors(fmap, X, K, W, H):
+    """fref = NN gather at the identity pose (model.py:74-97 conventions), [N, C] like fmap."""
+    p = project_pixels(np.eye(3), np.zeros(3), X, K)
+    inside = (p[:, 0] >= 0) & (p[:, 1] >= 0) & (p[:, 0] < W) & (p[:, 1] < H)
+    assert inside.all()
+    C, Hf, Wf = fmap.shape
+    rows = torch.as_tensor((p[:, 1].astype(np.int64) * Hf) // H, device=fmap.device)
+    cols = torch.as_tensor((p[:, 0].astype(np.int64) * Wf) // W, device=fmap.device)
+    return fmap[:, rows, cols].T.contiguous()
+
+
+def problem_inputs(N=512, C=256, Hf=240, Wf=320, seed=0, device="cuda"):
+    """Dict of one query's inputs: fmap [C,Hf,Wf] fp32 (device), fref [N,C] fp32 (device),
+    pts3d [N,3] fp64 (numpy), K, im_width, im_height, R0, t0."""
+    fmap = feature_map(C, Hf, Wf, seed, device)
+    X, K, W, H = scene(N, Hf, Wf, seed)
+    fref = reference_descriptors(fmap, X, K, W, H)
+    return dict(fmap=fmap, fref=fref, pts3d=X, K=K, im_width=W, im_height=H, R0=rot_z(1.0),
+                t0=np.array([0.05, -0.03, 0.10]))

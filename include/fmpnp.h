@@ -1,0 +1,161 @@
+/*
+ * fmpnp.h -- C ABI of libfmpnp.so, the MI355X (gfx950) feature-metric PnP refiner.
+ *
+ * Drop-in boundary for the reference's hot path (aunagar/FeatureMetric-PnP):
+ *
+ *   fmpnp_refine_batch / fmpnp_refine_batch_async
+ *       replace sparseFeaturePnP.forward          featurePnP/model.py:245-494
+ *       (and, with FMPNP_MODE_COMPUTE_COST,
+ *        sparseFeaturePnP.compute_cost            featurePnP/model.py:216-243)
+ *       -- the LM loop, the losses of          featurePnP/helpers/utils.py:15-78,
+ *          optimizer_step                       featurePnP/model.py:37-72,
+ *          indexing_ / points_within_image      featurePnP/model.py:74-117,
+ *          ratio_threshold_feature_errors       featurePnP/model.py:120-129,
+ *          so3exp_map                           featurePnP/helpers/utils.py:209-221.
+ *   fmpnp_pack_features
+ *       replaces sobel_filter + the fp64 cast   featurePnP/helpers/utils.py:81-104,
+ *                                               optimize_feature_pnp.py:57,61
+ *       (fused Sobel + channels-last [H][W][3][C] packing).
+ *   fmpnp_gather_reference
+ *       replaces the per-point fref gather       optimize_feature_pnp.py:51-56.
+ *
+ * Conventions: plain pointers and sizes, no torch types.  Feature / point
+ * buffers are caller-owned DEVICE memory; results and traces of the
+ * synchronous entry points are host memory.  Every entry point returns 0 on
+ * success, a negative FMPNP_E* code for invalid arguments, or a positive
+ * hipError_t; nothing throws.  One call per stream at a time; calls on
+ * distinct streams / devices are independent.  Multi-GPU = one call per device.
+ */
+#ifndef FMPNP_H
+#define FMPNP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FMPNP_ABI_VERSION 1
+
+/* robust losses, featurePnP/helpers/utils.py:15-78 */
+typedef enum {
+    FMPNP_SQUARED = 0,        /* squared_loss          :16-17 */
+    FMPNP_HUBER = 1,          /* huber_loss            :20-29 */
+    FMPNP_CAUCHY = 2,         /* cauchy_loss = barron(alpha=0)   :32-34 */
+    FMPNP_GEMAN_MCCLURE = 3,  /* geman_mcclure = barron(alpha=-2) :37-38 */
+    FMPNP_BARRON = 4          /* barron_loss(x, alpha) :40-78 */
+} fmpnp_loss;
+
+typedef enum {
+    FMPNP_NEAREST = 0,   /* the reference: round(K P / z) - 1, floor rescale (model.py:88-89,306-308) */
+    FMPNP_BILINEAR = 1   /* extension: 2x2 bilinear taps of f, gx, gy */
+} fmpnp_sampling;
+
+typedef enum { FMPNP_F32 = 0, FMPNP_F64 = 1 } fmpnp_dtype;
+
+typedef enum {
+    FMPNP_MODE_FORWARD = 0,       /* sparseFeaturePnP.forward */
+    FMPNP_MODE_COMPUTE_COST = 1   /* sparseFeaturePnP.compute_cost at (R0, t0) */
+} fmpnp_mode;
+
+/* per-problem status bits (fmpnp_result.status) */
+#define FMPNP_STATUS_OK 0
+#define FMPNP_STATUS_NO_SUPPORT 1        /* no point inside the image at (R0,t0): model.py:316-320 */
+#define FMPNP_STATUS_NAN 2               /* NaN step: model.py:411-413 (reference: NameError) */
+#define FMPNP_STATUS_NO_SUPPORT_TRIAL 4  /* no point inside at a trial pose: model.py:441-445 */
+#define FMPNP_STATUS_SYNC_TIMEOUT 8      /* internal: a cross-workgroup exchange timed out */
+
+/* argument errors (negative return codes) */
+#define FMPNP_EINVAL -1
+#define FMPNP_EALIGN -2
+#define FMPNP_ENOMEM -3
+#define FMPNP_ETOOBIG -4
+#define FMPNP_ENODEV -5
+
+typedef struct {
+    int mode;               /* fmpnp_mode */
+    int n_iters;            /* sparseFeaturePnP(n_iters) */
+    double lambda0;         /* sparseFeaturePnP(lambda_), default 0.01 */
+    int use_ratio;          /* ratio_threshold is not None */
+    double ratio_threshold; /* keep |rho| < max|rho| * thr */
+    int loss;               /* fmpnp_loss */
+    double barron_alpha;    /* FMPNP_BARRON only */
+    int sampling;           /* fmpnp_sampling */
+    int dtype;              /* fmpnp_dtype of the packed features and fref */
+    int wgs_per_problem;    /* workgroups cooperating on one problem; 0 = auto */
+    int max_teams;          /* cap on concurrently resident problem teams; 0 = auto */
+} fmpnp_options;
+
+typedef struct {
+    const void *feat;       /* device, [Hf][Wf][3][cstride] of dtype: planes f, gx, gy */
+    const void *fref;       /* device, [N][ld_ref] of dtype; columns [c_begin, c_end) used */
+    const double *pts3d;    /* device, [N][3] fp64 */
+    int Hf, Wf, cstride, c_begin, c_end, ld_ref, N;
+    int im_width, im_height;        /* image size in pixels (forward's im_width/im_height) */
+    double K[9], R0[9], t0[3];      /* row-major */
+} fmpnp_problem;
+
+typedef struct {
+    double R[9], t[3];      /* returned pose (R_best/t_best, or the current pose on early exit) */
+    double initial_cost;    /* mean rho at (R0,t0) (forward i==0 / compute_cost); NaN if none */
+    double best_cost;       /* best_cost_ (NaN when never set) */
+    double final_lambda, final_lr;
+    int best_num_inliers;   /* best_num_inliers_ (-1 when never set) */
+    int n_evals;            /* tracked evaluations: 1 + trials */
+    int n_steps;            /* optimizer steps taken */
+    int n_accepted;
+    int status;             /* FMPNP_STATUS_* bits */
+    int has_best;           /* best_cost_ was set */
+} fmpnp_result;
+
+typedef struct {            /* one tracked evaluation (model.track_, model.py:170-176) */
+    double R[9], t[3];
+    double cost;            /* mean rho at this pose */
+    double lambda_after, lr_after;
+    int n_supported, n_kept, accepted;
+} fmpnp_trace_entry;
+
+/* library identity / device check */
+int fmpnp_abi_version(void);
+const char *fmpnp_build_info(void);
+int fmpnp_device_check(int device); /* 0 if `device` is a gfx950 the library can run on */
+
+/* Fused Sobel (3x3, unnormalised unless sobel_normalized -> /8; zero or replicate
+ * padding) + channels-last pack: chw [C][H][W] (dtype_in) -> out [H][W][3][cstride]
+ * (dtype_out).  When gx_chw/gy_chw are non-NULL they are packed as given instead of
+ * computing the Sobel (forward() receives its gradients from the caller). */
+int fmpnp_pack_features(const void *chw, const void *gx_chw, const void *gy_chw, int dtype_in, int C, int H,
+                        int W, void *out, int dtype_out, int cstride, int sobel_normalized,
+                        int sobel_replicate_pad, void *hip_stream);
+
+/* fref gather of optimize_feature_pnp.py:51-56: for each of the N reference
+ * inliers (x, y) (device [N][2] fp64), row = trunc(y * W_ref / img1),
+ * col = trunc(x * H_ref / img0) of ref_chw [C][H_ref][W_ref] -> out [N][ld_out]. */
+int fmpnp_gather_reference(const void *ref_chw, int dtype_in, int C, int H_ref, int W_ref,
+                           const double *ref_inliers, int N, int img0, int img1, void *out, int dtype_out,
+                           int ld_out, void *hip_stream);
+
+/* Device workspace needed by fmpnp_refine_batch_async for n problems. */
+size_t fmpnp_workspace_size(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt);
+
+/* Asynchronous batched refinement: descriptors, results and trace in DEVICE
+ * memory; nothing is synchronised.  probs_host (may be NULL) is only read to
+ * size the launch; when NULL, max_N must bound every problem's N. */
+int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem *probs_host, int n, int max_N,
+                             const fmpnp_options *opt, fmpnp_result *results_dev, fmpnp_trace_entry *trace_dev,
+                             int trace_stride, void *workspace, size_t workspace_bytes, void *hip_stream);
+
+/* Synchronous convenience: host descriptors in, host results (and optional
+ * trace, [n][trace_stride] entries) out.  Uploads descriptors, launches on
+ * hip_stream and waits for that stream. */
+int fmpnp_refine_batch(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt, fmpnp_result *results,
+                       fmpnp_trace_entry *trace, int trace_stride, void *hip_stream);
+
+/* Last launch geometry of this thread (for benches / tests). */
+int fmpnp_last_launch(int *teams, int *wgs_per_problem, int *grid, int *lds_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FMPNP_H */

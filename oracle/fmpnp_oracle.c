@@ -456,10 +456,11 @@ void orc_sobel(const double *x, int C, int H, int W, double *gx, double *gy)
 }
 
 /* Batch of independent forwards, OpenMP over problems (the CPU baseline). */
-int orc_forward_batch(const orc_problem *pbs, int n, const orc_options *op, orc_result *res)
+int orc_forward_batch(const orc_problem *pbs, int n, const orc_options *op, orc_result *res, int nthreads)
 {
     int err = 0;
-#pragma omp parallel for schedule(dynamic, 1) reduction(| : err)
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : err) num_threads(nthreads)
     for (int i = 0; i < n; ++i) err |= orc_forward(pbs + i, op, res + i, NULL) != 0;
     return err ? -1 : 0;
 }

@@ -1,0 +1,8 @@
+#!/bin/bash
+# GPU bench: short bench.py run (+ optional rocprofv3 kernel stats), from the repo root.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?
+tail -5 gpurun_out/bench.err; cat gpurun_out/bench.json
+exit $rc
