@@ -21,12 +21,12 @@ namespace {
 
 struct Plan {
     int G = 1, teams = 1, teams_pad = 8, gw = 8, grid = 8, nc_max = 1, max_n = 0;
-    int tex_bytes = 0, rec_bytes = 0, lds = 0;
-    bool vec = true;
+    int mmax = 0, lds = 0;
     size_t ws_counters = 0, ws_partials = 0, ws_max = 0, ws_total = 0;
 };
 
 thread_local Plan g_last;
+unsigned long long *g_stamps = nullptr;  // debug phase stamps for the next launches
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -49,14 +49,6 @@ int validate(const fmpnp_problem *probs, int n, const fmpnp_options *opt) {
     return 0;
 }
 
-bool vec_ok(const fmpnp_problem &p, int dtype) {
-    const int V = dtype == FMPNP_F64 ? 2 : 4;
-    const int es = elem_size(dtype);
-    auto al = [&](const void *ptr) { return ((uintptr_t)ptr % 16) == 0; };
-    return al(p.feat) && al(p.fref) && p.cstride % V == 0 && p.ld_ref % V == 0 && p.c_begin % V == 0 &&
-           (p.c_end - p.c_begin) % V == 0 && es * V == 16;
-}
-
 int device_cus(int *ncu) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -70,59 +62,50 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     if (rc) return rc;
     Plan P;
     P.max_n = 0;
-    P.vec = true;
-    for (int i = 0; i < n; ++i) {
-        P.max_n = std::max(P.max_n, probs[i].N);
-        if (probs[i].N > 0 && !vec_ok(probs[i], opt->dtype)) P.vec = false;
-    }
+    for (int i = 0; i < n; ++i) P.max_n = std::max(P.max_n, probs[i].N);
     P.nc_max = std::max(1, (P.max_n + CH - 1) / CH);
     int ncu = 256;
     rc = device_cus(&ncu);
     if (rc) return rc;
-    // workgroups per problem: enough workgroups in flight to cover the chip (about two per
-    // CU), never more than the chunks of the largest problem, and few enough points per
-    // workgroup that its records fit a 64 KiB LDS budget.
-    const int lds_budget = 64 * 1024;
+    const int lds_cu = 160 * 1024;  // LDS per CU
     auto lds_for = [&](int G) {
-        int m = ((P.nc_max + G - 1) / G) * CH;
-        int tex = (int)align_up((size_t)m * 4, 16);
-        int rec = m * RECW * 8;
-        int part = G == 1 ? P.nc_max * NV * 8 : 0;
-        return lds_fixed_bytes() + tex + rec + part;
+        const int m = ((P.nc_max + G - 1) / G) * CH;
+        return lds_fixed_bytes() + (int)lm_dyn_lds_bytes(m, P.nc_max);
     };
+    // resident workgroups per CU (VGPR and LDS limits).  Hardware admission of 256-thread
+    // blocks is also bounded by SGPRs: floor(800 / (ceil(sgpr/16)*16 + 16)) >= 6 for any
+    // kernel (<= 112 SGPRs incl. VCC), and the API over-reports only above that
+    // (MI355X_MICROARCH.md, Residency) -> min(api, 6).
+    auto occupancy = [&](int lds) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lm_kernel_ptr(opt->dtype), NT, lds) != hipSuccess)
+            return 1;
+        return std::max(1, std::min(nb, 6));
+    };
+    // workgroups per problem: the fewest that put at least one workgroup on every CU
+    // (each extra team member adds a cross-workgroup exchange per evaluation), bounded by
+    // the chunks of the largest problem and by what fits in LDS at the resulting density.
     int G;
     if (opt->wgs_per_problem > 0) {
         G = std::min(opt->wgs_per_problem, P.nc_max);
     } else {
-        int target = 2 * ncu;
-        G = n > 0 ? (target + n - 1) / n : 1;
+        G = n > 0 ? (ncu + n - 1) / n : 1;
         G = std::max(1, std::min(G, P.nc_max));
     }
     G = std::min(G, MAX_G);
-    while (G < std::min(P.nc_max, MAX_G) && lds_for(G) > lds_budget) ++G;
-    if (lds_for(G) > 160 * 1024) return FMPNP_ETOOBIG;
+    while (G < std::min(P.nc_max, MAX_G) && lds_for(G) > lds_cu) ++G;
+    if (lds_for(G) > lds_cu) return FMPNP_ETOOBIG;
     P.G = G;
-    int m = ((P.nc_max + G - 1) / G) * CH;
-    P.tex_bytes = (int)align_up((size_t)m * 4, 16);
-    P.rec_bytes = m * RECW * 8;
+    P.mmax = ((P.nc_max + G - 1) / G) * CH;
     P.lds = lds_for(G);
-    // resident capacity: every workgroup of a team must be co-resident (teams spin on each
-    // other).  Occupancy API minus one block per CU of margin (it can over-report by one).
-    int per_cu = 1;
-    {
-        int nb = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lm_kernel_ptr(opt->dtype), NT, P.lds);
-        if (e != hipSuccess) return (int)e;
-        per_cu = nb > 1 ? nb - 1 : 1;
-        per_cu = std::min(per_cu, 4);
-    }
+    const int per_cu = occupancy(P.lds);
     long cap = (long)ncu * per_cu;
     if (G == 1) cap = std::max(cap, (long)n);  // no cross-workgroup waits: any grid is safe
     long max_teams = cap / G;
     if (opt->max_teams > 0) max_teams = std::min<long>(max_teams, opt->max_teams);
     // teams are padded to a multiple of the mapping group (8, the XCD count, or fewer
     // teams) for the XCD-aware blockIdx mapping; the padded grid stays within the
-    // resident capacity
+    // resident capacity whenever team members wait on each other (G > 1)
     long teams = std::min<long>(std::max(n, 1), max_teams);
     auto padded = [](long t) { long gw = t >= 8 ? 8 : t; return ((t + gw - 1) / gw) * gw; };
     while (teams > 1 && G > 1 && padded(teams) * G > cap) --teams;
@@ -230,9 +213,11 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
     a.counters = (unsigned *)ws;
     a.partials = (double *)(ws + P.ws_counters);
     a.maxslots = (double *)(ws + P.ws_counters + P.ws_partials);
-    a.tex_bytes = P.tex_bytes;
-    a.rec_bytes = P.rec_bytes;
+    a.mmax = P.mmax;
+    a.stamps = g_stamps;
     hipError_t e = hipMemsetAsync(a.counters, 0, P.ws_counters, s);
+    if (e != hipSuccess) return (int)e;
+    e = hipMemsetAsync(results_dev, 0, sizeof(fmpnp_result) * (size_t)n, s);  // texel_gathers accumulate
     if (e != hipSuccess) return (int)e;
     e = launch_lm(a, opt->dtype, P.grid, (size_t)P.lds, s);
     g_last = P;
@@ -293,6 +278,11 @@ int fmpnp_refine_batch(const fmpnp_problem *probs_host, int n, const fmpnp_optio
     }
     e = hipStreamSynchronize(s);
     return (int)e;
+}
+
+int fmpnp_debug_stamps(unsigned long long *device_buf) {
+    g_stamps = device_buf;
+    return 0;
 }
 
 int fmpnp_last_launch(int *teams, int *wgs_per_problem, int *grid, int *lds_bytes) {

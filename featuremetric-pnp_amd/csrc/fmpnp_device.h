@@ -37,6 +37,14 @@ __device__ __forceinline__ void loss_eval(int loss, double alpha, double x, doub
     } else if (alpha == 2.0) {                                          // :51-52
         rho = x;
         d1 = 1.0;
+    } else if (alpha == -2.0) {
+        // Geman-McClure: beta_safe = 4, alpha_safe = -2 -> rho = -4 (b^-1 - 1), rho' = b^-2 with
+        // b = x/4 + 1.  b^-1 is the correctly rounded 1/b (what a correctly rounded pow returns);
+        // b^-2 as (1/b)^2 is within 2 ulp of pow -- only the weights see it.
+        const double b = x / 4.0 + 1.0;
+        const double r = 1.0 / b;
+        rho = -4.0 * (r - 1.0);
+        d1 = r * r;
     } else {                                                            // :58-68
         double beta_safe = fabs(alpha - 2.0);
         beta_safe = beta_safe < kEpsF32 ? kEpsF32 : beta_safe;

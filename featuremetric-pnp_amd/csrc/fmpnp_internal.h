@@ -7,12 +7,15 @@
 
 namespace fmpnp {
 
-constexpr int NT = 256;         // threads per workgroup (4 waves)
+constexpr int NT = 1024;        // threads per workgroup of the LM kernel (16 waves)
 constexpr int CH = 16;          // points per reduction chunk (fixed: results do not depend on G)
 constexpr int NV = 32;          // reduced vector: 21 H + 6 g + rho + kept + supported + 2 pad
 constexpr int NGRP = NT / 16;   // 16-lane gather groups per workgroup
 constexpr int RECW = 8;         // per-point record: 6 channel sums + rho + rho'
 constexpr int MAX_G = 64;       // workgroups per problem
+#ifndef FMPNP_LM_WAVES_PER_SIMD
+#define FMPNP_LM_WAVES_PER_SIMD 4   // LM kernel occupancy target: <= 128 VGPRs -> 4 workgroups per CU
+#endif
 
 // Kernel arguments (by value).
 struct LaunchArgs {
@@ -26,11 +29,13 @@ struct LaunchArgs {
     unsigned *counters;           // [teams_pad][16], zeroed every launch
     double *partials;             // [teams][2][nc_max][NV]
     double *maxslots;             // [teams][2][G]
-    int tex_bytes, rec_bytes;     // dynamic LDS carve
+    int mmax;                     // max points per workgroup (multiple of CH): dynamic LDS carve
+    unsigned long long *stamps;   // debug: [grid][8] phase cycle totals, or null
 };
 
-// Fixed LDS head: LMState + sync flag + per-wave maxima (sized generously, 16-B aligned).
-__host__ __device__ constexpr int lds_fixed_bytes() { return 1536; }
+// Fixed LDS head: the LM state + per-problem context (sized generously, 16-B aligned).
+__host__ __device__ constexpr int lds_fixed_bytes() { return 12288; }
+size_t lm_dyn_lds_bytes(int mmax, int nc_max);
 
 hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream);
 const void *lm_kernel_ptr(int dtype);

@@ -21,6 +21,7 @@
 
 namespace fmpnp {
 
+constexpr int PK_NT = 256;   // threads per workgroup of the pack kernels
 constexpr int PK_CB = 64;    // channels per tile
 constexpr int PK_XW = 64;    // columns per tile
 constexpr int PK_RS = 8;     // rows per tile
@@ -37,7 +38,7 @@ __device__ __forceinline__ void load_row(const Tin *__restrict__ src, int C, int
     int yy = y;
     bool row_ok = (y >= 0 && y < H);
     if (!row_ok && replicate) { yy = y < 0 ? 0 : H - 1; row_ok = true; }
-    for (int e = threadIdx.x; e < PK_CB * ncol; e += NT) {
+    for (int e = threadIdx.x; e < PK_CB * ncol; e += PK_NT) {
         int cc = e / ncol, xx = e - cc * ncol;
         int c = c0 + cc, x = x0 - 1 + xx;
         Tin v = 0;
@@ -52,7 +53,7 @@ __device__ __forceinline__ void load_row(const Tin *__restrict__ src, int C, int
 }
 
 template <typename Tin, typename Tout, bool GIVEN>
-__global__ __launch_bounds__(NT) void pack_kernel(const Tin *__restrict__ chw, const Tin *__restrict__ gxc,
+__global__ __launch_bounds__(PK_NT) void pack_kernel(const Tin *__restrict__ chw, const Tin *__restrict__ gxc,
                                                   const Tin *__restrict__ gyc, int C, int H, int W,
                                                   Tout *__restrict__ out, int cs, int normalized, int replicate) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -78,7 +79,7 @@ __global__ __launch_bounds__(NT) void pack_kernel(const Tin *__restrict__ chw, c
         }
         __syncthreads();
         if (c < C) {
-            for (int xi = xg; xi < PK_XW; xi += NT / 64) {
+            for (int xi = xg; xi < PK_XW; xi += PK_NT / 64) {
                 const int x = x0 + xi;
                 if (x >= W) break;
                 double f, gx, gy;
@@ -117,10 +118,10 @@ static hipError_t pack_t(const void *chw, const void *gx, const void *gy, int C,
     dim3 grid((C + PK_CB - 1) / PK_CB, (W + PK_XW - 1) / PK_XW, (H + PK_RS - 1) / PK_RS);
     size_t lds = 3 * PK_CB * PK_LD * sizeof(Tin);
     if (gx) {
-        hipLaunchKernelGGL((pack_kernel<Tin, Tout, true>), grid, dim3(NT), lds, stream, (const Tin *)chw,
+        hipLaunchKernelGGL((pack_kernel<Tin, Tout, true>), grid, dim3(PK_NT), lds, stream, (const Tin *)chw,
                            (const Tin *)gx, (const Tin *)gy, C, H, W, (Tout *)out, cs, normalized, replicate);
     } else {
-        hipLaunchKernelGGL((pack_kernel<Tin, Tout, false>), grid, dim3(NT), lds, stream, (const Tin *)chw,
+        hipLaunchKernelGGL((pack_kernel<Tin, Tout, false>), grid, dim3(PK_NT), lds, stream, (const Tin *)chw,
                            (const Tin *)nullptr, (const Tin *)nullptr, C, H, W, (Tout *)out, cs, normalized,
                            replicate);
     }
@@ -142,11 +143,11 @@ hipError_t launch_pack(const void *chw, const void *gx, const void *gy, int dtyp
 // ref2d = int(relative_shape * (x, y)) truncates toward zero, then flip -> (row, col) =
 // (trunc(y * W_ref/img1), trunc(x * H_ref/img0)).  One thread per (point, channel).
 template <typename Tin, typename Tout>
-__global__ __launch_bounds__(NT) void gather_ref_kernel(const Tin *__restrict__ ref, int C, int H, int W,
+__global__ __launch_bounds__(PK_NT) void gather_ref_kernel(const Tin *__restrict__ ref, int C, int H, int W,
                                                         const double *__restrict__ inl, int N, int img0, int img1,
                                                         Tout *__restrict__ out, int ld, int *__restrict__ err) {
     const long total = (long)N * C;
-    for (long e = blockIdx.x * (long)NT + threadIdx.x; e < total; e += (long)gridDim.x * NT) {
+    for (long e = blockIdx.x * (long)PK_NT + threadIdx.x; e < total; e += (long)gridDim.x * PK_NT) {
         const int n = (int)(e / C), c = (int)(e % C);
         const double rel0 = (double)H / (double)img0, rel1 = (double)W / (double)img1;
         const double x = inl[2 * n], y = inl[2 * n + 1];
@@ -169,10 +170,10 @@ template <typename Tin, typename Tout>
 static hipError_t gather_t(const void *ref, int C, int H, int W, const double *inl, int N, int img0, int img1,
                            void *out, int ld, int *err, hipStream_t stream) {
     long total = (long)N * C;
-    int grid = (int)((total + NT - 1) / NT);
+    int grid = (int)((total + PK_NT - 1) / PK_NT);
     if (grid > 4096) grid = 4096;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((gather_ref_kernel<Tin, Tout>), dim3(grid), dim3(NT), 0, stream, (const Tin *)ref, C, H, W, inl,
+    hipLaunchKernelGGL((gather_ref_kernel<Tin, Tout>), dim3(grid), dim3(PK_NT), 0, stream, (const Tin *)ref, C, H, W, inl,
                        N, img0, img1, (Tout *)out, ld, err);
     return hipGetLastError();
 }

@@ -26,7 +26,7 @@ class Options(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int), ("n_iters", ctypes.c_int), ("lambda0", ctypes.c_double),
                 ("use_ratio", ctypes.c_int), ("ratio_threshold", ctypes.c_double), ("loss", ctypes.c_int),
                 ("barron_alpha", ctypes.c_double), ("sampling", ctypes.c_int), ("dtype", ctypes.c_int),
-                ("wgs_per_problem", ctypes.c_int), ("max_teams", ctypes.c_int)]
+                ("wgs_per_problem", ctypes.c_int), ("max_teams", ctypes.c_int), ("no_memo", ctypes.c_int)]
 
 
 class Problem(ctypes.Structure):
@@ -41,7 +41,8 @@ class Result(ctypes.Structure):
     _fields_ = [("R", ctypes.c_double * 9), ("t", ctypes.c_double * 3), ("initial_cost", ctypes.c_double),
                 ("best_cost", ctypes.c_double), ("final_lambda", ctypes.c_double), ("final_lr", ctypes.c_double),
                 ("best_num_inliers", ctypes.c_int), ("n_evals", ctypes.c_int), ("n_steps", ctypes.c_int),
-                ("n_accepted", ctypes.c_int), ("status", ctypes.c_int), ("has_best", ctypes.c_int)]
+                ("n_accepted", ctypes.c_int), ("status", ctypes.c_int), ("has_best", ctypes.c_int),
+                ("texel_gathers", ctypes.c_longlong)]
 
 
 class TraceEntry(ctypes.Structure):
@@ -52,7 +53,7 @@ class TraceEntry(ctypes.Structure):
 
 EXPORTS = ["fmpnp_abi_version", "fmpnp_build_info", "fmpnp_device_check", "fmpnp_pack_features",
            "fmpnp_gather_reference", "fmpnp_workspace_size", "fmpnp_refine_batch_async", "fmpnp_refine_batch",
-           "fmpnp_last_launch"]
+           "fmpnp_last_launch", "fmpnp_debug_stamps"]
 
 _LIB = None
 

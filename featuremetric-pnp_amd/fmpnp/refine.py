@@ -183,7 +183,7 @@ def make_problem(feats, fref, pts3d, K, im_width, im_height, R0, t0, c_begin=0, 
 
 
 def make_options(n_iters, lambda0=0.01, loss=_lib.SQUARED, barron_alpha=0.0, ratio_threshold=None,
-                 dtype=_lib.F32, mode=_lib.MODE_FORWARD, wgs_per_problem=0, max_teams=0):
+                 dtype=_lib.F32, mode=_lib.MODE_FORWARD, wgs_per_problem=0, max_teams=0, memoize=True):
     o = _lib.Options()
     o.mode = int(mode)
     o.n_iters = int(n_iters)
@@ -196,6 +196,7 @@ def make_options(n_iters, lambda0=0.01, loss=_lib.SQUARED, barron_alpha=0.0, rat
     o.dtype = int(dtype)
     o.wgs_per_problem = int(wgs_per_problem)
     o.max_teams = int(max_teams)
+    o.no_memo = 0 if memoize else 1
     return o
 
 
@@ -203,7 +204,8 @@ def _result_dict(r):
     return dict(R=np.array(r.R[:]).reshape(3, 3), t=np.array(r.t[:]), initial_cost=r.initial_cost,
                 best_cost=r.best_cost, final_lambda=r.final_lambda, final_lr=r.final_lr,
                 best_num_inliers=r.best_num_inliers, n_evals=r.n_evals, n_steps=r.n_steps,
-                n_accepted=r.n_accepted, status=r.status, has_best=bool(r.has_best))
+                n_accepted=r.n_accepted, status=r.status, has_best=bool(r.has_best),
+                texel_gathers=int(r.texel_gathers))
 
 
 def _trace_dict(entries, n):

@@ -1,0 +1,44 @@
+"""Multi-GPU sharding of independent refinement problems.
+
+Queries are independent, so a batch is cut into contiguous blocks, one per rank
+(one process per GPU, the reference's own scale-out is the same query slicing,
+run.py:38-39).  No collective touches the data path; the only exchange is the
+optional final gather of the small per-query results (12 doubles + counters).
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n_total, rank, world):
+    """Contiguous block [lo, hi) of n_total problems for `rank` of `world` (sizes differ by <= 1)."""
+    base, extra = divmod(int(n_total), int(world))
+    lo = rank * base + min(rank, extra)
+    hi = lo + base + (1 if rank < extra else 0)
+    return lo, hi
+
+
+def refine_sharded(make_problem, n_total, refine_fn, group=None):
+    """Refine problems [lo, hi) of this rank and all-gather the per-problem results in
+    global order.  make_problem(i) builds problem i; refine_fn(list) returns one result
+    dict per problem."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    lo, hi = shard_range(n_total, rank, world)
+    local = refine_fn([make_problem(i) for i in range(lo, hi)]) if hi > lo else []
+    if world == 1:
+        return local
+    parts = [None] * world
+    dist.all_gather_object(parts, (lo, local), group=group)
+    out = []
+    for _, res in sorted(parts, key=lambda x: x[0]):
+        out.extend(res)
+    return out
+
+
+def max_over_ranks(x, device=None, group=None):
+    """Max of a float over ranks (bench timing)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())

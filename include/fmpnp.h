@@ -85,6 +85,9 @@ typedef struct {
     int dtype;              /* fmpnp_dtype of the packed features and fref */
     int wgs_per_problem;    /* workgroups cooperating on one problem; 0 = auto */
     int max_teams;          /* cap on concurrently resident problem teams; 0 = auto */
+    int no_memo;            /* 1: re-gather every point's texel at every evaluation (the
+                               reference's data movement); 0 (default): re-gather only points
+                               whose texel changed -- bit-identical results */
 } fmpnp_options;
 
 typedef struct {
@@ -107,6 +110,9 @@ typedef struct {
     int n_accepted;
     int status;             /* FMPNP_STATUS_* bits */
     int has_best;           /* best_cost_ was set */
+    long long texel_gathers; /* point-texel gathers actually read from memory by the problem's
+                                first workgroup (a texel is re-read only when a point's pixel
+                                changes: the channel sums of an unchanged texel are reused) */
 } fmpnp_result;
 
 typedef struct {            /* one tracked evaluation (model.track_, model.py:170-176) */
@@ -151,6 +157,10 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
  * hip_stream and waits for that stream. */
 int fmpnp_refine_batch(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt, fmpnp_result *results,
                        fmpnp_trace_entry *trace, int trace_stride, void *hip_stream);
+
+/* Debug: when device_buf != NULL, later LM launches write per-workgroup phase cycle
+ * totals (s_memtime) to device_buf[grid][8]; NULL switches it off. */
+int fmpnp_debug_stamps(unsigned long long *device_buf);
 
 /* Last launch geometry of this thread (for benches / tests). */
 int fmpnp_last_launch(int *teams, int *wgs_per_problem, int *grid, int *lds_bytes);

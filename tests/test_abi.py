@@ -1,0 +1,75 @@
+"""The C ABI (include/fmpnp.h): library loads without a GPU, exports every declared
+entry point, and the ctypes mirror of every struct matches the C layout."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from fmpnp import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "fmpnp.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w[\w\s\*]*?\b(fmpnp_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_abi():
+    fns = declared_functions()
+    for f in ("fmpnp_refine_batch", "fmpnp_refine_batch_async", "fmpnp_pack_features", "fmpnp_gather_reference",
+              "fmpnp_workspace_size", "fmpnp_abi_version"):
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.load()
+    missing = [f for f in declared_functions() if not hasattr(L, f)]
+    assert not missing, missing
+    assert L.fmpnp_abi_version() == 1
+    assert b"gfx950" in L.fmpnp_build_info()
+
+
+def test_library_is_a_gfx950_code_object():
+    """The fat binary embeds an amdgcn code object for gfx950 (and nothing else to fall back to)."""
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert b"gfx942" not in blob and b"gfx90a" not in blob
+
+
+STRUCTS = {"fmpnp_options": _lib.Options, "fmpnp_problem": _lib.Problem, "fmpnp_result": _lib.Result,
+           "fmpnp_trace_entry": _lib.TraceEntry}
+
+
+@pytest.mark.parametrize("name", sorted(STRUCTS))
+def test_struct_layout_matches_c(name):
+    cls = STRUCTS[name]
+    lines = [f'printf("%zu\\n", sizeof({name}));']
+    for fname, _ in cls._fields_:
+        lines.append(f'printf("%zu\\n", offsetof({name}, {fname}));')
+    prog = "#include <stdio.h>\n#include <stddef.h>\n#include \"fmpnp.h\"\nint main(void){\n" + "\n".join(lines) + \
+           "\nreturn 0;}\n"
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(prog)
+        exe = os.path.join(d, "t")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        vals = [int(x) for x in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
+    assert vals[0] == ctypes.sizeof(cls)
+    for (fname, _), off in zip(cls._fields_, vals[1:]):
+        assert getattr(cls, fname).offset == off, fname
+
+
+def test_entry_points_reject_bad_arguments_without_a_device():
+    """Argument validation happens before any device call: no GPU needed."""
+    L = _lib.load()
+    assert L.fmpnp_pack_features(None, None, None, 0, 1, 1, 1, None, 0, 1, 0, 0, None) == -1
+    assert L.fmpnp_gather_reference(None, 0, 1, 1, 1, None, 1, 1, 1, None, 0, 1, None) == -1
+    o = _lib.Options()
+    o.dtype = 7
+    assert L.fmpnp_refine_batch(None, 1, ctypes.byref(o), None, None, 0, None) == -1

@@ -1,0 +1,87 @@
+"""Multi-process (world_size 2, gloo, CPU) test of the query sharding used on N GPUs.
+
+The compute of each shard here is the CPU oracle (test infrastructure) standing in
+for the device refiner: this test covers the distribution plumbing -- contiguous
+blocks, all-gather in global order, max-over-ranks timing -- not the kernel.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from fmpnp.shard import shard_range
+
+
+def test_shard_range_covers_all():
+    for n in (0, 1, 7, 1024, 1025):
+        for w in (1, 2, 3, 8):
+            blocks = [shard_range(n, r, w) for r in range(w)]
+            assert blocks[0][0] == 0 and blocks[-1][1] == n
+            for (a, b), (c, d) in zip(blocks, blocks[1:]):
+                assert b == c
+            sizes = [b - a for a, b in blocks]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def _problem(i):
+    import oracle.oracle as orc
+    from golden_io import case, maps64
+    names = ["gm_c16", "cauchy_c16", "odd_geom_gm", "behind_camera_gm", "huber_c16"]
+    inp, meta, _ = case(names[i % len(names)])
+    f, gx, gy = maps64(inp, orc.sobel)
+    t0 = np.asarray(inp["t0"]) * (1.0 + 0.1 * i)
+    return orc.make_problem(inp["pts3d"], inp["fref"], f, gx, gy, inp["K"], inp["im_width"], inp["im_height"],
+                            inp["R0"], t0)
+
+
+def _refine(probs):
+    import oracle.oracle as orc
+    opts = orc.make_options(8, 0.01, "geman_mcclure")
+    return [dict(R=r["R"].tolist(), t=r["t"].tolist(), best_cost=r["best_cost"])
+            for r in orc.forward_batch(probs, opts, 1)]
+
+
+def _worker(rank, world, port, n, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "featuremetric-pnp_amd"), os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from fmpnp.shard import max_over_ranks, refine_sharded
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = refine_sharded(_problem, n, _refine)
+    m = max_over_ranks(float(rank + 1))
+    if rank == 0:
+        q.put((res, m))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(240)
+def test_two_rank_gloo_matches_single_process():
+    n = 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res, m = q.get(timeout=200)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    single = _refine([_problem(i) for i in range(n)])
+    assert m == 2.0
+    assert len(res) == n
+    for a, b in zip(res, single):
+        assert a["R"] == b["R"] and a["t"] == b["t"] and a["best_cost"] == b["best_cost"]

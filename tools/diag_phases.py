@@ -1,0 +1,38 @@
+"""Phase shares of the LM kernel from the debug s_memtime stamps (fmpnp_debug_stamps)."""
+import ctypes, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "featuremetric-pnp_amd")]
+import numpy as np, torch
+from fmpnp import _lib, refine as rf, synth
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+wgs = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+dev = torch.device("cuda", 0)
+probs = []
+for q in range(B):
+    inp = synth.problem_inputs(512, 256, 240, 320, seed=q, device=dev)
+    feats = rf.pack_features(inp["fmap"], storage=torch.float32, device=dev)
+    probs.append(rf.make_problem(feats, inp["fref"], inp["pts3d"], inp["K"], inp["im_width"], inp["im_height"], inp["R0"], inp["t0"]))
+opts = rf.make_options(50, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32, wgs_per_problem=wgs)
+ab = rf.AsyncBatch(probs, opts)
+ab.launch(); torch.cuda.synchronize()
+L = _lib.load()
+L.fmpnp_debug_stamps.argtypes = [ctypes.c_void_p]
+info = _lib.last_launch()
+st = torch.zeros(info["grid"] * 8, dtype=torch.int64, device=dev)
+L.fmpnp_debug_stamps(ctypes.c_void_p(st.data_ptr()))
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record(); ab.launch(); e1.record(); torch.cuda.synchronize()
+L.fmpnp_debug_stamps(None)
+e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e2.record(); ab.launch(); e3.record(); torch.cuda.synchronize()
+ph = st.view(-1, 8).cpu().numpy().astype(np.float64)
+res = ab.results()
+g = sum(r["texel_gathers"] for r in res)
+full = sum(r["n_evals"] for r in res) * 512
+print(f"texel gathers {g} of {full} point-evals ({100.0 * g / max(full, 1):.1f} %)")
+names = ["A0 proj", "A gather", "B1 loss", "B2 contrib", "combine", "LM state", "LU solve", "pose+sync"]
+tot = ph.sum(0)
+print(f"B={B} launch={info} stamped launch {e0.elapsed_time(e1):.3f} ms, plain launch {e2.elapsed_time(e3):.3f} ms")
+for k in range(8):
+    print(f"  {names[k]:12s} {100 * tot[k] / tot.sum():6.2f} %   mean per WG {ph[:, k].mean() / 1e3:10.1f} kcyc")
