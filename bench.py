@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=512, help="queries in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-extras", action="store_true", help="skip single-query / pack / CPU legs")
+    ap.add_argument("--no-nomemo", action="store_true", help="skip the memoisation-off comparison launch")
     return ap.parse_args()
 
 
@@ -125,6 +126,36 @@ def main():
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
     algo_bytes = B * ITERS * B_ITER
     achieved = algo_bytes / avg_kernel_s
+    # bytes the memoised kernel actually gathers: 16C per point-texel gather (f, gx, gy, fref
+    # fp32) + the fp64 points read once per query
+    gathers = int(sum(r["texel_gathers"] for r in res))
+    gathered_bytes = gathers * 16 * C + B * N_PTS * 24
+    n_evals = int(sum(r["n_evals"] for r in res))
+
+    # the same launch with memoisation off: every point's texel re-read at every evaluation,
+    # i.e. the reference's data movement -- the HBM-bound form of the loop
+    nm = {}
+    if not args.no_nomemo:
+        opts_nm = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32, wgs_per_problem=args.wgs,
+                                  memoize=False)
+        batch_nm = rf.AsyncBatch(probs, opts_nm)
+        batch_nm.launch()
+        torch.cuda.synchronize()
+        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = max(1, min(args.steps, 5))
+        s_ev.record(stream)
+        for _ in range(reps):
+            batch_nm.launch()
+        e_ev.record(stream)
+        torch.cuda.synchronize()
+        nm_s = s_ev.elapsed_time(e_ev) / reps / 1e3
+        res_nm = batch_nm.results()
+        same = all(np.array_equal(a["R"], b["R"]) and np.array_equal(a["t"], b["t"]) for a, b in zip(res, res_nm))
+        nm_bytes = int(sum(r["texel_gathers"] for r in res_nm)) * 16 * C + B * N_PTS * 24
+        nm = {"ms_per_launch": round(nm_s * 1e3, 4), "pose_refinements_per_s": round(B / nm_s, 1),
+              "gathered_bytes_per_launch": nm_bytes, "achieved_GB_per_s": round(nm_bytes / nm_s / 1e9, 1),
+              "frac": round(nm_bytes / nm_s / HBM_PEAK, 4), "poses_bit_identical_to_memoised": bool(same)}
+        del batch_nm
 
     extras = {}
     if rank == 0 and not args.no_extras:
@@ -158,7 +189,16 @@ def main():
                          "traffic": traffic,
                          "kernel": "fmpnp::lm_kernel<float>", "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
                          "algorithmic_bytes_per_launch": algo_bytes,
-                         "bytes_rule": "B * iters * N*(16C+24) (f, gx, gy, fref fp32 at one texel + fp64 point)"},
+                         "bytes_rule": "SURVEY.md 8d: B * iters * N*(16C+24) (f, gx, gy, fref fp32 at one "
+                                       "texel + fp64 point per GN iteration)",
+                         "gathered_bytes_per_launch": gathered_bytes,
+                         "gathered_GB_per_s": round(gathered_bytes / avg_kernel_s / 1e9, 1),
+                         "texel_gathers_per_point_eval": round(gathers / max(1, n_evals * N_PTS), 4),
+                         "note": "achieved counts the reference's data movement; the kernel re-reads a "
+                                 "texel only when a point's pixel changed (bit-identical), so achieved > "
+                                 "peak is possible; gathered_* is what it actually reads, no_memo the "
+                                 "HBM-bound form"},
+            "no_memo": nm,
             "statuses": statuses,
         }
         out.update(extras)

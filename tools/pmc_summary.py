@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Summarise a tools/gpu_profile.sh run: per-kernel stats (kernel trace) and the HBM
+bytes per LM launch from the FETCH_SIZE / WRITE_SIZE passes.
+
+FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB.  On gfx950 FETCH_SIZE
+reports half of the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM section):
+it is doubled here; WRITE_SIZE is taken as is.
+
+usage: pmc_summary.py <prof_dir> <batch> <out.json>
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def rows(pattern):
+    out = []
+    for path in glob.glob(pattern, recursive=True):
+        with open(path, newline="") as f:
+            out.extend(csv.DictReader(f))
+    return out
+
+
+def counter_avg(prof, sub, name, kernel_key):
+    vals = {}
+    for r in rows(os.path.join(prof, sub, "**", "*counter_collection.csv")):
+        if kernel_key in r.get("Kernel_Name", "") and r.get("Counter_Name") == name:
+            d = r.get("Dispatch_Id") or r.get("Correlation_Id")
+            vals[d] = vals.get(d, 0.0) + float(r["Counter_Value"])
+    if not vals:
+        return None, 0
+    return sum(vals.values()) / len(vals), len(vals)
+
+
+def main():
+    prof, batch, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
+    key = "lm_kernel"
+    stats = [r for r in rows(os.path.join(prof, "trace", "**", "*kernel_stats.csv"))]
+    lm = [r for r in stats if key in r.get("Name", "")]
+    fetch_kib, nf = counter_avg(prof, "pmc_fetch", "FETCH_SIZE", key)
+    write_kib, nw = counter_avg(prof, "pmc_write", "WRITE_SIZE", key)
+    summary = {
+        "batch": batch,
+        "kernel": lm[0]["Name"] if lm else None,
+        "kernel_calls": int(lm[0]["Calls"]) if lm else None,
+        "kernel_avg_ns": float(lm[0]["AverageNs"]) if lm else None,
+        "fetch_size_kib_raw": fetch_kib,
+        "write_size_kib": write_kib,
+        "dispatches_counted": [nf, nw],
+        "hbm_bytes_per_launch": (None if fetch_kib is None or write_kib is None
+                                 else int(2 * fetch_kib * 1024 + write_kib * 1024)),
+        "correction": "FETCH_SIZE x2 (gfx950 wide-read halving), KiB -> bytes",
+        "all_kernels": [{k: r[k] for k in ("Name", "Calls", "AverageNs", "Percentage") if k in r} for r in stats],
+    }
+    with open(out, "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps({k: v for k, v in summary.items() if k != "all_kernels"}))
+
+
+if __name__ == "__main__":
+    main()
