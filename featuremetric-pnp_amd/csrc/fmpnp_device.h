@@ -13,6 +13,70 @@ template <typename T> struct V16;
 template <> struct V16<float> { typedef float4 type; static constexpr int n = 4; };
 template <> struct V16<double> { typedef double2 type; static constexpr int n = 2; };
 
+// ---------------------------------------------------------------------------
+// Cross-lane exchange of doubles without the LDS path (ds_bpermute): DPP inside a row
+// of 16 lanes, v_permlane{16,32}_swap across rows (gfx950).  Partners used by the
+// reductions: xor 1, xor 2 (quad_perm), i^7 within 8 (row_half_mirror), i^15 within 16
+// (row_mirror); each flips the bit being split and keeps every higher bit.
+// ---------------------------------------------------------------------------
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_MIRROR8 = 0x141, DPP_MIRROR16 = 0x140;
+
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ double join64(unsigned lo, unsigned hi) {
+    return __longlong_as_double(((long long)hi << 32) | lo);
+}
+
+// Rows (0,1) and (2,3) exchange: odd rows of a swap with even rows of b.  Returns
+// (a', b') -- even rows: (own a, partner's a); odd rows: (partner's b, own b).
+__device__ __forceinline__ void swap16(double &a, double &b) {
+    const long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+    const auto l = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)y, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap((unsigned)(x >> 32), (unsigned)(y >> 32), false, false);
+    a = join64(l[0], h[0]);
+    b = join64(l[1], h[1]);
+}
+// Same across the two 32-lane halves of the wave.
+__device__ __forceinline__ void swap32(double &a, double &b) {
+    const long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+    const auto l = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)y, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap((unsigned)(x >> 32), (unsigned)(y >> 32), false, false);
+    a = join64(l[0], h[0]);
+    b = join64(l[1], h[1]);
+}
+
+// One halving step of a transposed reduction with an in-row DPP partner: the lane keeps
+// `hi` when its split bit is set, else `lo`, and adds the partner's copy of the same.
+template <int CTRL>
+__device__ __forceinline__ double tstep(double lo, double hi, bool bit) {
+    const double send = bit ? lo : hi, keep = bit ? hi : lo;
+    return keep + dpp64<CTRL>(send);
+}
+
+// NaN-propagating max (the reference's torch.max over |rho| propagates NaN)
+__device__ __forceinline__ double nanmax(double a, double b) {
+    return (isnan(b) || b > a) ? (isnan(a) ? a : b) : a;
+}
+// max over the 64 lanes of a wave (order-free: exact)
+__device__ __forceinline__ double wave_nanmax(double v) {
+    v = nanmax(v, dpp64<DPP_XOR1>(v));
+    v = nanmax(v, dpp64<DPP_XOR2>(v));
+    v = nanmax(v, dpp64<DPP_MIRROR8>(v));
+    v = nanmax(v, dpp64<DPP_MIRROR16>(v));
+    double a = v, b = v;
+    swap16(a, b);
+    v = nanmax(a, b);
+    a = v, b = v;
+    swap32(a, b);
+    return nanmax(a, b);
+}
+
 // torch.finfo(torch.float).eps as the reference uses it (helpers/utils.py:25,58)
 constexpr double kEpsF32 = 1.1920928955078125e-07;
 

@@ -349,28 +349,21 @@ __device__ __forceinline__ void gather_half(const T *__restrict__ t, const T *__
 }
 
 // Transposed reduction of 8 values over the 32 lanes of a half-wave: halving exchanges
-// at offsets 16, 8, 4 then butterflies at 2, 1 (9 shuffles).  Returns the half's total of
-// value index 4*b4 + 2*b3 + b2 of the lane; only equal indices are ever added.
+// at bit 4 (permlane16 swap), bit 3 (row mirror), bit 2 (half-row mirror), then
+// butterflies at bits 1, 0 -- no LDS traffic.  Returns the half's total of value index
+// 4*b4 + 2*b3 + b2 of the lane; only equal indices are ever added.
 __device__ __forceinline__ double reduce8_in32(double v[8], int lane) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const bool hi = lane & 16;
-        const double send = hi ? v[i] : v[i + 4], keep = hi ? v[i + 4] : v[i];
-        v[i] = keep + __shfl_xor(send, 16);
+        double a = v[i], b = v[i + 4];
+        swap16(a, b);  // even rows keep index i, odd rows i + 4
+        v[i] = a + b;
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const bool hi = lane & 8;
-        const double send = hi ? v[i] : v[i + 2], keep = hi ? v[i + 2] : v[i];
-        v[i] = keep + __shfl_xor(send, 8);
-    }
-    {
-        const bool hi = lane & 4;
-        const double send = hi ? v[0] : v[1], keep = hi ? v[1] : v[0];
-        v[0] = keep + __shfl_xor(send, 4);
-    }
-    v[0] = v[0] + __shfl_xor(v[0], 2);
-    return v[0] + __shfl_xor(v[0], 1);
+    for (int i = 0; i < 2; ++i) v[i] = tstep<DPP_MIRROR16>(v[i], v[i + 2], lane & 8);
+    v[0] = tstep<DPP_MIRROR8>(v[0], v[1], lane & 4);
+    v[0] = v[0] + dpp64<DPP_XOR2>(v[0]);
+    return v[0] + dpp64<DPP_XOR1>(v[0]);
 }
 
 template <typename T>
@@ -407,30 +400,16 @@ __device__ __forceinline__ void phase_gather(int mmax) {
     }
 }
 
-// Transposed reduction of 8 values over the 16 lanes of a group: 7 shuffles instead
-// of 8 x 4.  Returns the group total of value index (4*b3 + 2*b2 + b1) of l16.
+// Transposed reduction of 8 values over the 16 lanes of a row (DPP only): halving at
+// bits 3, 2, 1 then a butterfly at bit 0.  Returns the row total of value index
+// 4*b3 + 2*b2 + b1 of l16.
 __device__ __forceinline__ double reduce8_in16(double v[8], int l16) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        bool hi = l16 & 8;
-        double send = hi ? v[i] : v[i + 4];
-        double keep = hi ? v[i + 4] : v[i];
-        v[i] = keep + __shfl_xor(send, 8);
-    }
+    for (int i = 0; i < 4; ++i) v[i] = tstep<DPP_MIRROR16>(v[i], v[i + 4], l16 & 8);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        bool hi = l16 & 4;
-        double send = hi ? v[i] : v[i + 2];
-        double keep = hi ? v[i + 2] : v[i];
-        v[i] = keep + __shfl_xor(send, 4);
-    }
-    {
-        bool hi = l16 & 2;
-        double send = hi ? v[0] : v[1];
-        double keep = hi ? v[1] : v[0];
-        v[0] = keep + __shfl_xor(send, 2);
-    }
-    return v[0] + __shfl_xor(v[0], 1);
+    for (int i = 0; i < 2; ++i) v[i] = tstep<DPP_MIRROR8>(v[i], v[i + 2], l16 & 4);
+    v[0] = tstep<DPP_XOR2>(v[0], v[1], l16 & 2);
+    return v[0] + dpp64<DPP_XOR1>(v[0]);
 }
 
 // ---------------------------------------------------------------------------
@@ -460,10 +439,7 @@ __device__ __forceinline__ bool phase_loss(int mmax) {
     }
     if (!c.use_ratio) return true;
     // wave max then workgroup max (max is order-independent: exact)
-    for (int o = 32; o > 0; o >>= 1) {
-        const double other = __shfl_xor(lmax, o);
-        if (isnan(other) || other > lmax) lmax = isnan(lmax) ? lmax : other;
-    }
+    lmax = wave_nanmax(lmax);
     if (lane == 0) st.wg_max[wave] = lmax;
     __syncthreads();
     if (tid == 0) {
@@ -600,18 +576,30 @@ __device__ __forceinline__ bool phase_combine(int mmax) {
         st.tree[q][j] = acc;
     }
     __syncthreads();
-    if (tid < NV) {
-        double t[NQ];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) t[q] = st.tree[q][tid];
-#pragma unroll
-        for (int w = 1; w < NQ; w *= 2)
-#pragma unroll
-            for (int q = 0; q < NQ; q += 2 * w) t[q] = t[q] + t[q + w];
-        st.tot[tid] = t[0];
-    }
-    __syncthreads();
     return true;
+}
+
+// Final level of the ordered sum on wave 0 (no barrier: the LM update that reads the
+// totals runs on the same wave): lane l sums rows 16*(l>>5) .. +15 of value l&31 with a
+// fixed pairwise tree, the two halves are added across the wave -- the same tree as a
+// single pairwise tree over the NQ = 32 rows.
+static_assert(NQ == 32, "final tree assumes 32 rows");
+__device__ __forceinline__ void combine_final_wave() {
+    LMState &st = S();
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    double t[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t[q] = st.tree[16 * h + q][j];
+#pragma unroll
+    for (int w = 1; w < 16; w *= 2)
+#pragma unroll
+        for (int q = 0; q < 16; q += 2 * w) t[q] = t[q] + t[q + w];
+    double a = t[0], b = t[0];
+    swap32(a, b);  // low half: (own, partner); high half: (partner, own)
+    const double tot = a + b;  // rows 0..15 + rows 16..31 in both halves
+    if (lane < NV) st.tot[lane] = tot;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
 }
 
 // ---------------------------------------------------------------------------
@@ -648,6 +636,7 @@ __device__ __forceinline__ void lm_step_rows(const double *Hu, const double *g, 
     double inv[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
+        const double rj = 1.0 / A[j];  // every row's candidate pivot reciprocal, off the critical path
         int p = j;
         double best = fabs(rlane(A[j], lane_at[j]));
 #pragma unroll
@@ -666,9 +655,9 @@ __device__ __forceinline__ void lm_step_rows(const double *Hu, const double *g, 
         else if (lane == lj) pos = p;
         double prow[6];
 #pragma unroll
-        for (int c = j; c < 6; ++c) prow[c] = rlane(A[c], lp);
+        for (int c = j + 1; c < 6; ++c) prow[c] = rlane(A[c], lp);
         const double pb = rlane(b, lp);
-        const double iv = 1.0 / prow[j];
+        const double iv = rlane(rj, lp);  // = 1 / A[p][j], computed before the pivot was known
         inv[j] = iv;
         if (pos > j && pos < 6) {
             const double m = A[j] * iv;
@@ -690,6 +679,59 @@ __device__ __forceinline__ void lm_step_rows(const double *Hu, const double *g, 
 }
 
 // ---------------------------------------------------------------------------
+// Fast path of the damped solve: H + lambda diag(diag(H) + 1e-9) is symmetric positive
+// definite whenever lambda > 0 (H = sum rho' J^T J with rho' > 0 for every loss), so an
+// LDL^T factorisation needs no pivoting and no cross-lane traffic: every lane of wave 0
+// runs the same ~160 register-resident fp64 instructions.  The reference's LU solve
+// (model.py:51,61) and this one agree to rounding (cond(H) * eps, far inside the pose
+// tolerance; tests/test_gpu_parity.py).  Returns false -- and the caller falls back to
+// the pivoted LU -- when a pivot is not positive (lambda = 0 on a singular H, NaN).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool ldlt_step(const double *Hu, const double *g, double lambda, double lr,
+                                          double delta[6]) {
+    double a[6][6];  // lower triangle used: a[i][j], i >= j
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) a[i][j] = Hu[tri6(j, i)];
+    if (lambda != 0.0) {
+#pragma unroll
+        for (int j = 0; j < 6; ++j) a[j][j] = a[j][j] + (a[j][j] + 1e-9) * lambda;
+    }
+    double b[6], inv[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) b[i] = g[i];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        ok &= a[j][j] > 0.0;  // false for NaN
+        inv[j] = 1.0 / a[j][j];
+        double u[6];
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) u[i] = a[i][j];
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) {
+            const double l = u[i] * inv[j];
+#pragma unroll
+            for (int c = j + 1; c <= i; ++c) a[i][c] = fma(-l, u[c], a[i][c]);
+            b[i] = fma(-l, b[j], b[i]);  // forward substitution L y = g, folded in
+            a[i][j] = l;
+        }
+    }
+    double x[6];
+#pragma unroll
+    for (int j = 5; j >= 0; --j) {
+        double v = b[j] * inv[j];
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) v = fma(-a[i][j], x[i], v);
+        x[j] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) delta[i] = -lr * x[i];
+    return ok;
+}
+
+// ---------------------------------------------------------------------------
 // LM state machine (model.py:300-486) on wave 0: every lane computes the same uniform
 // state (lane 0 alone writes it back) and the wave solves the 6x6 system together.
 // Every team member computes the same from identical totals.
@@ -697,7 +739,8 @@ __device__ __forceinline__ void lm_step_rows(const double *Hu, const double *g, 
 __device__ __forceinline__ void lm_update_wave() {
     LMState &st = S();
     const Ctx &c = st.c;
-    const bool w0 = (threadIdx.x & 63) == 0;
+    const int lane = threadIdx.x & 63;
+    const bool w0 = lane == 0;
     const int nsup = (int)st.tot[29];
     const int kept = (int)st.tot[28];
     const double cost = st.tot[27] / st.tot[28];  // torch mean of an empty tensor = NaN
@@ -736,6 +779,20 @@ __device__ __forceinline__ void lm_update_wave() {
     }
     // the evaluated pose becomes current and its normal equations the linearisation
     const bool take = first || accepted;
+    const bool new_best = !first && accepted && cost < st.best;
+    // pose / linearisation copies: one element per lane
+    if (new_best && lane < 12) {
+        if (lane < 9) st.Rb[lane] = st.Re[lane];
+        else st.tb[lane - 9] = st.te[lane - 9];
+    }
+    if (take && lane < 12) {
+        if (lane < 9) st.R[lane] = st.Re[lane];
+        else st.t[lane - 9] = st.te[lane - 9];
+    }
+    if (take && lane < 27) {
+        if (lane < 21) st.Hc[lane] = st.tot[lane];
+        else st.gc[lane - 21] = st.tot[lane];
+    }
     if (w0) {
         if (first) {  // model.py:347-359
             st.prev = st.best = st.initial = cost;
@@ -743,19 +800,11 @@ __device__ __forceinline__ void lm_update_wave() {
             st.has_best = 1;
         } else if (accepted) {  // model.py:477-486
             st.n_accepted++;
-            if (cost < st.best) {
-                for (int k = 0; k < 9; ++k) st.Rb[k] = st.Re[k];
-                for (int k = 0; k < 3; ++k) st.tb[k] = st.te[k];
+            if (new_best) {
                 st.best_inl = kept;
                 st.best = cost;
             }
             st.prev = cost;
-        }
-        if (take) {
-            for (int k = 0; k < 9; ++k) st.R[k] = st.Re[k];
-            for (int k = 0; k < 3; ++k) st.t[k] = st.te[k];
-            for (int k = 0; k < 21; ++k) st.Hc[k] = st.tot[k];
-            for (int k = 0; k < 6; ++k) st.gc[k] = st.tot[21 + k];
         }
         st.lambda = lambda;
         st.lr = lr;
@@ -779,7 +828,10 @@ __device__ __forceinline__ void lm_update_wave() {
     // next step from the linearisation at the current pose (model.py:408-426)
     double delta[6];
     dbg_stamp(5);  // LM bookkeeping
-    lm_step_rows(take ? st.tot : st.Hc, take ? st.tot + 21 : st.gc, lambda, lr, delta);
+    {
+        const double *Hu = take ? st.tot : st.Hc, *gv = take ? st.tot + 21 : st.gc;
+        if (!ldlt_step(Hu, gv, lambda, lr, delta)) lm_step_rows(Hu, gv, lambda, lr, delta);
+    }
     dbg_stamp(6);  // 6x6 solve
     bool bad = false;
 #pragma unroll
@@ -874,8 +926,11 @@ __global__ __launch_bounds__(NT, FMPNP_LM_WAVES_PER_SIMD) void lm_kernel(LaunchA
             phase_contrib(mmax);
             STAMP(3);
             if (!phase_combine(mmax)) break;
-            STAMP(4);
-            if (tid < 64) lm_update_wave();
+            if (tid < 64) {
+                combine_final_wave();
+                STAMP(4);
+                lm_update_wave();
+            }
             __syncthreads();
             STAMP(7);  // pose update + barrier
         }

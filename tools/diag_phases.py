@@ -24,8 +24,11 @@ L.fmpnp_debug_stamps(ctypes.c_void_p(st.data_ptr()))
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record(); ab.launch(); e1.record(); torch.cuda.synchronize()
 L.fmpnp_debug_stamps(None)
-e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-e2.record(); ab.launch(); e3.record(); torch.cuda.synchronize()
+plain = []
+for _ in range(10):
+    e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e2.record(); ab.launch(); e3.record(); torch.cuda.synchronize()
+    plain.append(e2.elapsed_time(e3))
 ph = st.view(-1, 8).cpu().numpy().astype(np.float64)
 res = ab.results()
 g = sum(r["texel_gathers"] for r in res)
@@ -33,6 +36,6 @@ full = sum(r["n_evals"] for r in res) * 512
 print(f"texel gathers {g} of {full} point-evals ({100.0 * g / max(full, 1):.1f} %)")
 names = ["A0 proj", "A gather", "B1 loss", "B2 contrib", "combine", "LM state", "LU solve", "pose+sync"]
 tot = ph.sum(0)
-print(f"B={B} launch={info} stamped launch {e0.elapsed_time(e1):.3f} ms, plain launch {e2.elapsed_time(e3):.3f} ms")
+print(f"B={B} launch={info} stamped launch {e0.elapsed_time(e1):.3f} ms, plain launch median {np.median(plain):.3f} ms (min {min(plain):.3f}) -> {B / np.median(plain) * 1e3:.0f} /s")
 for k in range(8):
     print(f"  {names[k]:12s} {100 * tot[k] / tot.sum():6.2f} %   mean per WG {ph[:, k].mean() / 1e3:10.1f} kcyc")
