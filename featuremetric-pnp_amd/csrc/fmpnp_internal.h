@@ -11,6 +11,7 @@ constexpr int NT = 1024;        // threads per workgroup of the LM kernel (16 wa
 constexpr int CH = 16;          // points per reduction chunk (fixed: results do not depend on G)
 constexpr int NV = 32;          // reduced vector: 21 H + 6 g + rho + kept + supported + 2 pad
 constexpr int NGRP = NT / 16;   // 16-lane gather groups per workgroup
+constexpr int NSTAMP = 12;      // debug phase-stamp slots: 8 phases + eval-0 proj/gather/loss/contrib
 constexpr int RECW = 8;         // per-point record: 6 channel sums + rho + rho'
 constexpr int MAX_G = 64;       // workgroups per problem
 #ifndef FMPNP_LM_WAVES_PER_SIMD
@@ -30,7 +31,7 @@ struct LaunchArgs {
     double *partials;             // [teams][2][nc_max][NV]
     double *maxslots;             // [teams][2][G]
     int mmax;                     // max points per workgroup (multiple of CH): dynamic LDS carve
-    unsigned long long *stamps;   // debug: [grid][8] phase cycle totals, or null
+    unsigned long long *stamps;   // debug: [grid][NSTAMP] phase cycle totals, or null
 };
 
 // Fixed LDS head: the LM state + per-problem context (sized generously, 16-B aligned).

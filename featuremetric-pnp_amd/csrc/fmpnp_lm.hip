@@ -83,7 +83,7 @@ struct LMState {
     long long gathers;      // texel gathers done for the current problem
     double wg_max[NT / 64];
     double tree[NT / NV][NV];  // ordered-sum tree level
-    unsigned long long stamp_t, stamp_ph[8];  // debug phase stamps (lane 0)
+    unsigned long long stamp_t, stamp_ph[NSTAMP];  // debug phase stamps (lane 0)
     Ctx c;
 };
 static_assert(sizeof(LMState) <= lds_fixed_bytes(), "LDS head too small");
@@ -321,22 +321,42 @@ __device__ __forceinline__ void acc6(double a[8], double f, double r, double gx,
     a[5] = fma(gy, gy, a[5]);
 }
 
+template <typename VT>
+__device__ __forceinline__ VT gload(const void *p) {  // global (not flat) 16-byte load
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *reinterpret_cast<const __attribute__((address_space(1))) VT *>(reinterpret_cast<uintptr_t>(p));
+#else
+    return *reinterpret_cast<const VT *>(p);  // host pass: never executed
+#endif
+}
+
 template <typename T, bool VEC>
 __device__ __forceinline__ void gather_half(const T *__restrict__ t, const T *__restrict__ rf, int cs, int cb,
                                             int ce, int l32, double a[8]) {
     using VT = typename V16<T>::type;
     constexpr int V = V16<T>::n;
     if constexpr (VEC) {
-#pragma unroll 2
-        for (int c = cb + l32 * V; c < ce; c += 32 * V) {
-            const VT f = *reinterpret_cast<const VT *>(t + c);
-            const VT x = *reinterpret_cast<const VT *>(t + cs + c);
-            const VT y = *reinterpret_cast<const VT *>(t + 2 * cs + c);
-            const VT q = *reinterpret_cast<const VT *>(rf + c);
-            const T *pf = reinterpret_cast<const T *>(&f), *px = reinterpret_cast<const T *>(&x);
-            const T *py = reinterpret_cast<const T *>(&y), *pr = reinterpret_cast<const T *>(&q);
+        // two rounds per trip, all eight loads issued before the first use (one round trip
+        // for C <= 64 V); a missing second round reads round one again and adds exact zeros
+        for (int c = cb + l32 * V; c < ce; c += 64 * V) {
+            const bool has2 = c + 32 * V < ce;
+            const int c2 = has2 ? c + 32 * V : c;
+            const VT f0 = gload<VT>(t + c), x0 = gload<VT>(t + cs + c), y0 = gload<VT>(t + 2 * cs + c);
+            const VT q0 = gload<VT>(rf + c);
+            const VT f1 = gload<VT>(t + c2), x1 = gload<VT>(t + cs + c2), y1 = gload<VT>(t + 2 * cs + c2);
+            const VT q1 = gload<VT>(rf + c2);
+            const T *pf = reinterpret_cast<const T *>(&f0), *px = reinterpret_cast<const T *>(&x0);
+            const T *py = reinterpret_cast<const T *>(&y0), *pr = reinterpret_cast<const T *>(&q0);
 #pragma unroll
             for (int k = 0; k < V; ++k) acc6(a, (double)pf[k], (double)pr[k], (double)px[k], (double)py[k]);
+            const T *sf = reinterpret_cast<const T *>(&f1), *sx = reinterpret_cast<const T *>(&x1);
+            const T *sy = reinterpret_cast<const T *>(&y1), *sr = reinterpret_cast<const T *>(&q1);
+#pragma unroll
+            for (int k = 0; k < V; ++k) {
+                const double z = 0.0;
+                acc6(a, has2 ? (double)sf[k] : z, has2 ? (double)sr[k] : z, has2 ? (double)sx[k] : z,
+                     has2 ? (double)sy[k] : z);
+            }
         }
     } else {
         for (int c = cb + l32 * V; c < ce; c += 32 * V) {
@@ -902,13 +922,13 @@ __global__ __launch_bounds__(NT, FMPNP_LM_WAVES_PER_SIMD) void lm_kernel(LaunchA
     // optional phase stamps (debug: a.stamps != null): s_memtime deltas on lane 0 after barriers
     const bool stamps_on = a.stamps != nullptr;
     if (stamps_on && tid == 0) {
-        for (int k = 0; k < 8; ++k) st.stamp_ph[k] = 0;
+        for (int k = 0; k < NSTAMP; ++k) st.stamp_ph[k] = 0;
         st.stamp_t = __builtin_amdgcn_s_memtime();
     }
 #define STAMP(k)                                                \
     if (stamps_on && tid == 0) {                                \
         unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
-        st.stamp_ph[k] += now_ - st.stamp_t;                    \
+        st.stamp_ph[(k) < 4 && st.n_evals == 0 ? 8 + (k) : (k)] += now_ - st.stamp_t; \
         st.stamp_t = now_;                                      \
     }
 
@@ -937,7 +957,7 @@ __global__ __launch_bounds__(NT, FMPNP_LM_WAVES_PER_SIMD) void lm_kernel(LaunchA
         problem_end();
     }
     if (stamps_on && tid == 0)
-        for (int k = 0; k < 8; ++k) a.stamps[(size_t)blockIdx.x * 8 + k] = st.stamp_ph[k];
+        for (int k = 0; k < NSTAMP; ++k) a.stamps[(size_t)blockIdx.x * NSTAMP + k] = st.stamp_ph[k];
 #undef STAMP
 }
 

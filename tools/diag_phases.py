@@ -19,7 +19,7 @@ ab.launch(); torch.cuda.synchronize()
 L = _lib.load()
 L.fmpnp_debug_stamps.argtypes = [ctypes.c_void_p]
 info = _lib.last_launch()
-st = torch.zeros(info["grid"] * 8, dtype=torch.int64, device=dev)
+st = torch.zeros(info["grid"] * 12, dtype=torch.int64, device=dev)
 L.fmpnp_debug_stamps(ctypes.c_void_p(st.data_ptr()))
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record(); ab.launch(); e1.record(); torch.cuda.synchronize()
@@ -29,13 +29,14 @@ for _ in range(10):
     e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e2.record(); ab.launch(); e3.record(); torch.cuda.synchronize()
     plain.append(e2.elapsed_time(e3))
-ph = st.view(-1, 8).cpu().numpy().astype(np.float64)
+ph = st.view(-1, 12).cpu().numpy().astype(np.float64)
 res = ab.results()
 g = sum(r["texel_gathers"] for r in res)
 full = sum(r["n_evals"] for r in res) * 512
 print(f"texel gathers {g} of {full} point-evals ({100.0 * g / max(full, 1):.1f} %)")
-names = ["A0 proj", "A gather", "B1 loss", "B2 contrib", "combine", "LM state", "LU solve", "pose+sync"]
+names = ["A0 proj", "A gather", "B1 loss", "B2 contrib", "combine", "LM state", "LU solve", "pose+sync",
+         "eval0 proj", "eval0 gather", "eval0 loss", "eval0 contrib"]
 tot = ph.sum(0)
 print(f"B={B} launch={info} stamped launch {e0.elapsed_time(e1):.3f} ms, plain launch median {np.median(plain):.3f} ms (min {min(plain):.3f}) -> {B / np.median(plain) * 1e3:.0f} /s")
-for k in range(8):
+for k in range(12):
     print(f"  {names[k]:12s} {100 * tot[k] / tot.sum():6.2f} %   mean per WG {ph[:, k].mean() / 1e3:10.1f} kcyc")
