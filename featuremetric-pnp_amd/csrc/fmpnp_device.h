@@ -121,6 +121,25 @@ __device__ __forceinline__ void loss_eval(int loss, double alpha, double x, doub
     }
 }
 
+// Exact floor(a / d) for 0 <= a < 2^32, 1 <= d < 2^31 by an invariant multiplier
+// (Granlund & Montgomery 1994; "round-up" method with a 33-bit multiplier):
+// l = ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1, t = mulhi(m, a),
+// q = (t + ((a - t) >> 1)) >> (l - 1)   (l = 0: q = a).
+struct UDiv {
+    unsigned m;
+    int s1, s2;
+};
+__host__ __device__ inline UDiv udiv_make(unsigned d) {
+    int l = 0;
+    while ((1ull << l) < d) ++l;
+    const unsigned long long m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+    return UDiv{(unsigned)m, l ? 1 : 0, l ? l - 1 : 0};
+}
+__device__ __forceinline__ unsigned udiv(unsigned a, UDiv u) {
+    const unsigned t = __umulhi(u.m, a);
+    return (t + ((a - t) >> u.s1)) >> u.s2;
+}
+
 // P = R X + t exactly as torch.mm computes it for these shapes (sequential, no FMA):
 // the pixel rounding below must see the same bits as the reference (model.py:303).
 __device__ __forceinline__ void transform_pt(const double *R, const double *t, double X0, double X1, double X2,

@@ -7,15 +7,14 @@
 
 namespace fmpnp {
 
-constexpr int NT = 1024;        // threads per workgroup of the LM kernel (16 waves)
+constexpr int NT = 512;         // threads per workgroup of the LM kernel (8 waves)
 constexpr int CH = 16;          // points per reduction chunk (fixed: results do not depend on G)
 constexpr int NV = 32;          // reduced vector: 21 H + 6 g + rho + kept + supported + 2 pad
-constexpr int NGRP = NT / 16;   // 16-lane gather groups per workgroup
 constexpr int NSTAMP = 12;      // debug phase-stamp slots: 8 phases + eval-0 proj/gather/loss/contrib
 constexpr int RECW = 8;         // per-point record: 6 channel sums + rho + rho'
 constexpr int MAX_G = 64;       // workgroups per problem
 #ifndef FMPNP_LM_WAVES_PER_SIMD
-#define FMPNP_LM_WAVES_PER_SIMD 4   // LM kernel occupancy target: <= 128 VGPRs -> 4 workgroups per CU
+#define FMPNP_LM_WAVES_PER_SIMD 2   // LM kernel occupancy target: one 512-thread workgroup per CU, <= 256 VGPRs
 #endif
 
 // Kernel arguments (by value).
@@ -35,7 +34,7 @@ struct LaunchArgs {
 };
 
 // Fixed LDS head: the LM state + per-problem context (sized generously, 16-B aligned).
-__host__ __device__ constexpr int lds_fixed_bytes() { return 12288; }
+__host__ __device__ constexpr int lds_fixed_bytes() { return 4096; }
 size_t lm_dyn_lds_bytes(int mmax, int nc_max);
 
 hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream);

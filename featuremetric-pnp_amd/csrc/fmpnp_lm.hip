@@ -4,38 +4,36 @@
 // (sparseFeaturePnP.forward, featurePnP/model.py:245-494) on the device.
 //
 // Work decomposition
-//   * A "team" of G workgroups (256 threads each) owns one problem at a time;
+//   * A "team" of G workgroups (512 threads = 8 waves each) owns one problem at a time;
 //     teams walk the batch persistently (problem = team, team + T, ...).
-//   * Points are cut into chunks of CH = 16.  Workgroup s of a team owns a
-//     contiguous range of chunks.  Per evaluation it
-//       A0  projects its points (thread per point, fp64, exact pixel rounding),
-//       A   gathers f / gx / gy / fref at the nearest texel with one 16-lane group
-//           per point -- 16-byte loads of the channels-last [H][W][3][C] texel, so a
-//           point's channels are contiguous coalesced reads -- and reduces the six
-//           channel sums  sum e^2, sum gx e, sum gy e, sum gx^2, sum gx gy, sum gy^2
-//           in fp64 (the C x 6 Jacobian is never materialised: J = G A with the 2x6
-//           pose chain A, so J^T e = A^T (G^T e), J^T J = A^T (G^T G) A),
-//       B   turns each point's record into its 21 + 6 normal-equation entries, its
-//           rho and counters (thread per point) and reduces every chunk with a
-//           fixed transposed shuffle tree to one 32-double partial.
-//   * The chunk partials are summed by a fixed tree over CHUNK INDICES.  Results are
-//     therefore deterministic and independent of G: the LM accept test `new > prev`
-//     (model.py:469-472) compares costs that tie exactly whenever the pixel sets
-//     are equal, and a scheduling-dependent sum would break those ties.
+//   * Points are cut into chunks of CH = 16; workgroup s of a team owns a contiguous
+//     range of chunks, and wave w of the workgroup owns the 64-point blocks w, w+8, ...
+//     of that range.  Per evaluation a wave carries each of its blocks from projection
+//     to chunk partials with NO workgroup barrier:
+//       project  (lane per point, fp64, exact pixel rounding) -> texel offset, P;
+//       gather   the points whose texel changed (ballot), two per wave: each half-wave
+//                issues 16-byte loads of the channels-last [H][W][3][C] texel and fref
+//                and reduces the six channel sums  sum e^2, sum gx e, sum gy e, sum gx^2,
+//                sum gx gy, sum gy^2  in fp64 (the C x 6 Jacobian is never materialised:
+//                J = G A with the 2x6 pose chain A, so J^T e = A^T (G^T e),
+//                J^T J = A^T (G^T G) A); unchanged texels keep their sums (memoisation);
+//       loss + normal equations (lane per point) -> 21 + 6 entries, rho and counters,
+//                reduced per 16-point chunk by a fixed transposed DPP tree.
+//   * The chunk partials are summed by wave 0 with a fixed tree over CHUNK INDICES.  Results
+//     are therefore deterministic and independent of G: the LM accept test `new > prev`
+//     (model.py:469-472) compares costs that tie exactly whenever the pixel sets are
+//     equal, and a scheduling-dependent sum would break those ties.
 //   * G > 1: chunk partials go to a per-team slot with write-through (sc1) stores,
-//     every storing wave drains, one lane bumps the team's arrival counter, one
-//     lane polls it (bounded spin), one agent-scope acquire, then every
-//     workgroup re-reads all partials and runs the identical 6x6 solve + LM
-//     update redundantly (no second exchange).
-//   * One evaluation per iteration: the trial evaluation at (R', t') also
-//     produces that pose's normal equations.  On acceptance they are the next
-//     linearisation; on rejection the cached ones are reused -- bit-identical to
-//     the reference's recomputation at the unchanged pose (model.py:472-476).
-//
-// Code shape: every phase reads what it needs from LDS (the per-problem context `Ctx`
-// and the LM state) after a barrier, so no value stays live in registers from one
-// phase to the next; the 6x6 solve runs row-parallel on wave 0.  That keeps the
-// 1024-thread workgroup within 128 VGPRs.
+//     every storing wave drains, one lane bumps the team's arrival counter, one lane
+//     polls it (bounded spin), one agent-scope acquire; then wave 0 of every member
+//     reads all partials and runs the identical 6x6 solve + LM update (no second exchange).
+//   * One evaluation per iteration: the trial evaluation at (R', t') also produces that
+//     pose's normal equations.  On acceptance they are the next linearisation; on
+//     rejection the cached ones are reused -- bit-identical to the reference's
+//     recomputation at the unchanged pose (model.py:472-476).
+//   * The ratio test (model.py:324-336) needs max|rho| over the team before any point's
+//     weight is known: with it, loss values are parked in LDS, the maximum is exchanged,
+//     and a second pass over the blocks forms the normal equations.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -67,6 +65,7 @@ struct Ctx {
     const double *pts;
     double K[9];
     int p, N, Hf, Wf, cs, cb, ce, ld_ref, im_w, im_h, vec;
+    UDiv div_h, div_w;    // exact floor division by im_h, im_w (indexing_)
     int p0, M, c0, LC, NC;
 };
 
@@ -79,37 +78,33 @@ struct LMState {
     double lambda, lr, prev, best, initial, rho_max;
     int best_inl, n_evals, n_steps, n_accepted, status, done, has_best, ret_current;
     int abort_flag, sync_ok;
-    int ndirty;             // points whose texel changed this evaluation (gather list length)
-    long long gathers;      // texel gathers done for the current problem
     double wg_max[NT / 64];
-    double tree[NT / NV][NV];  // ordered-sum tree level
     unsigned long long stamp_t, stamp_ph[NSTAMP];  // debug phase stamps (lane 0)
     Ctx c;
 };
 static_assert(sizeof(LMState) <= lds_fixed_bytes(), "LDS head too small");
 
 __device__ __forceinline__ LMState &S() { return *reinterpret_cast<LMState *>(lm_lds); }
-// debug: add the cycles since the previous stamp to phase k (lane 0 of the workgroup only)
+// debug: add the cycles since the previous stamp to phase k (lane 0 of the workgroup only);
+// phases 0..3 of the first evaluation go to slots 8..11
 __device__ __forceinline__ void dbg_stamp(int k) {
     LMState &st = *reinterpret_cast<LMState *>(lm_lds);
     if (st.c.stamps_on && threadIdx.x == 0) {
         const unsigned long long now = __builtin_amdgcn_s_memtime();
-        st.stamp_ph[k] += now - st.stamp_t;
+        st.stamp_ph[k < 4 && st.n_evals == 0 ? 8 + k : k] += now - st.stamp_t;
         st.stamp_t = now;
     }
 }
 __device__ __forceinline__ unsigned char *dyn() { return lm_lds + lds_fixed_bytes(); }
 // dynamic carve (mmax = max local points, a multiple of CH):
-//   X[mmax][3], P[mmax][3], rec[mmax][RECW] doubles, tex[mmax] + list[mmax] ints, part[nc_max][NV] doubles
+//   X[mmax][3], rec[mmax][RECW] doubles, tex[mmax] ints (16-B padded), part[nc_max][NV] doubles
 __device__ __forceinline__ double *lds_X(int mmax) { return reinterpret_cast<double *>(dyn()); }
-__device__ __forceinline__ double *lds_P(int mmax) { return reinterpret_cast<double *>(dyn()) + 3 * mmax; }
-__device__ __forceinline__ double *lds_rec(int mmax) { return reinterpret_cast<double *>(dyn()) + 6 * mmax; }
+__device__ __forceinline__ double *lds_rec(int mmax) { return reinterpret_cast<double *>(dyn()) + 3 * mmax; }
 __device__ __forceinline__ int *lds_tex(int mmax) {
-    return reinterpret_cast<int *>(reinterpret_cast<double *>(dyn()) + (6 + RECW) * mmax);
+    return reinterpret_cast<int *>(reinterpret_cast<double *>(dyn()) + (3 + RECW) * mmax);
 }
-__device__ __forceinline__ int *lds_list(int mmax) { return lds_tex(mmax) + mmax; }
 __device__ __forceinline__ double *lds_part(int mmax) {
-    return reinterpret_cast<double *>(dyn()) + (6 + RECW) * mmax + mmax + 2;
+    return reinterpret_cast<double *>(dyn()) + (3 + RECW) * mmax + ((mmax + 3) / 4) * 2;
 }
 
 // so3exp_map (helpers/utils.py:209-221) and the update R' = dR R, t' = dR t + dt
@@ -146,44 +141,60 @@ __device__ __forceinline__ void pose_update(const double *R, const double *t, co
 }
 
 // ---------------------------------------------------------------------------
-// Cross-workgroup exchange inside a team (G > 1).  Payload is stored write-through
-// (sc1, agent-scope relaxed atomic stores); the arrival counter is monotonic within
-// a launch and zeroed by the launcher (hipMemsetAsync) before every launch.
+// Cross-workgroup exchange inside a team (G > 1), MI355X_MICROARCH.md "sc1 loads in place
+// of the acquire", first row: every byte handed off is stored write-through (sc1) and
+// read back with global sc1 loads; every storing wave drains (vmcnt(0)) before a workgroup
+// barrier, behind which ONE lane per workgroup adds to the team's arrival counter (agent
+// scope); the consumer is the polling wave itself (wave 0), which loads only after its
+// poll has matched -- no L1 invalidate, no second barrier.  The counter is monotonic
+// within a launch and zeroed by the launcher (hipMemsetAsync) before every launch.
+// One workgroup per CU (the planner's launch bounds), memory from hipMalloc.
 // ---------------------------------------------------------------------------
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+typedef __attribute__((address_space(1))) unsigned g_u32;
+#else
+typedef unsigned long long g_u64;  // host pass: never executed
+typedef unsigned g_u32;
+#endif
 __device__ __forceinline__ void st_sc1(double *p, double v) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), __double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<g_u64 *>(reinterpret_cast<uintptr_t>(p)), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ double ld_sc1(const double *p) {
-    return __longlong_as_double(__hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT));
+    return __longlong_as_double((long long)__hip_atomic_load(
+        reinterpret_cast<g_u64 *>(reinterpret_cast<uintptr_t>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-// Every thread calls this after its sc1 stores; on return S().c.epoch is the epoch
-// just completed.  Returns false on timeout.
-__device__ __forceinline__ bool team_sync() {
+// Every thread calls this after its sc1 stores: this workgroup's arrival for the next epoch.
+__device__ __forceinline__ void team_arrive() {
     LMState &st = S();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned ep = ++st.c.epoch;
-        const unsigned target = ep * (unsigned)st.c.G;
-        unsigned *counter = st.c.counter;
-        __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int ok = 1;
-        // bounded spin: give up after ~2 s of wall time (s_memrealtime ticks at 100 MHz)
+        ++st.c.epoch;
+        __hip_atomic_fetch_add(reinterpret_cast<g_u32 *>(reinterpret_cast<uintptr_t>(st.c.counter)), 1u,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Wave 0 (all its lanes) after team_arrive: thread 0 polls until every member has arrived
+// for the current epoch (bounded: ~2 s of wall time, s_memrealtime ticks at 100 MHz).
+// Returns false -- and raises the workgroup's abort flag -- on timeout.
+__device__ __forceinline__ bool team_wait() {
+    LMState &st = S();
+    int ok = 1;
+    if (threadIdx.x == 0) {
+        const unsigned target = st.c.epoch * (unsigned)st.c.G;
+        g_u32 *counter = reinterpret_cast<g_u32 *>(reinterpret_cast<uintptr_t>(st.c.counter));
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             __builtin_amdgcn_s_sleep(1);
             if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) { ok = 0; break; }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        st.sync_ok = ok;
         if (!ok) st.abort_flag = 1;
     }
-    __syncthreads();
-    return st.sync_ok != 0;
+    return __builtin_amdgcn_readfirstlane(ok) != 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -208,6 +219,8 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
         c.im_w = pb->im_width;
         c.im_h = pb->im_height;
         for (int k = 0; k < 9; ++k) c.K[k] = pb->K[k];
+        c.div_h = udiv_make((unsigned)c.im_h);
+        c.div_w = udiv_make((unsigned)c.im_w);
         c.NC = (c.N + CH - 1) / CH;
         c.c0 = (int)(((long)c.NC * c.s) / c.G);
         const int c1 = (int)(((long)c.NC * (c.s + 1)) / c.G);
@@ -227,8 +240,6 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
         st.ret_current = 0;
         st.done = c.dead || (c.mode != FMPNP_MODE_COMPUTE_COST && c.n_iters <= 0);
         st.abort_flag = 0;
-        st.ndirty = 0;
-        st.gathers = 0;
     }
     __syncthreads();
     // this workgroup's points -> LDS once per problem
@@ -264,43 +275,8 @@ __device__ __forceinline__ void problem_end() {
             r.status = st.status;
             r.has_best = st.has_best;
         }
-        // every team member adds its share (results are zeroed by the launcher)
-        atomicAdd(reinterpret_cast<unsigned long long *>(&st.c.results[st.c.p].texel_gathers),
-                  (unsigned long long)st.gathers);
     }
     __syncthreads();
-}
-
-// ---------------------------------------------------------------------------
-// A0: projection (thread per local point) -> texel offset + camera-frame point
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void phase_project(int mmax) {
-    LMState &st = S();
-    const Ctx &c = st.c;
-    const double *X = lds_X(mmax);
-    double *P = lds_P(mmax);
-    int *tex = lds_tex(mmax);
-    for (int i = threadIdx.x; i < c.M; i += NT) {
-        double Pc[3];
-        transform_pt(st.Re, st.te, X[3 * i], X[3 * i + 1], X[3 * i + 2], Pc);
-        int x, y;
-        int off = -1;
-        if (project_px(c.K, Pc, c.im_w, c.im_h, x, y)) {
-            // indexing_ (model.py:88-89): floor(y*Hf/H), floor(x*Wf/W), exact in integers
-            // y*Hf and x*Wf are exact in fp64, and a correctly rounded quotient of two
-            // integers floors to the integer quotient: exact, without a software int division
-            const int row = (int)floor(((double)y * (double)c.Hf) / (double)c.im_h);
-            const int col = (int)floor(((double)x * (double)c.Wf) / (double)c.im_w);
-            off = row * c.Wf + col;
-        }
-        // memoised gather: a point whose texel did not change keeps its record (the six
-        // channel sums depend only on the texel and the point's fixed descriptor)
-        if (off >= 0 && (off != tex[i] || c.no_memo)) lds_list(mmax)[atomicAdd(&st.ndirty, 1)] = i;
-        tex[i] = off;
-        P[3 * i] = Pc[0];
-        P[3 * i + 1] = Pc[1];
-        P[3 * i + 2] = Pc[2];
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -386,40 +362,6 @@ __device__ __forceinline__ double reduce8_in32(double v[8], int lane) {
     return v[0] + dpp64<DPP_XOR1>(v[0]);
 }
 
-template <typename T>
-__device__ __forceinline__ void phase_gather(int mmax) {
-    LMState &st = S();
-    const Ctx &c = st.c;
-    const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, half = tid >> 5;
-    constexpr int NH = NT / 32;
-    const int *tex = lds_tex(mmax);
-    double *rec = lds_rec(mmax);
-    const T *feat = reinterpret_cast<const T *>(c.feat);
-    const T *fref = reinterpret_cast<const T *>(c.fref);
-    const int cs = c.cs, cb = c.cb, ce = c.ce, p0 = c.p0, ld = c.ld_ref;
-    constexpr int V = V16<T>::n;
-    const bool vec = ((((uintptr_t)feat) | ((uintptr_t)fref)) & 15) == 0 && cs % V == 0 && ld % V == 0 &&
-                     cb % V == 0 && (ce - cb) % V == 0;
-    const int *list = lds_list(mmax);
-    const int nd = st.ndirty;
-    // every lane of a wave runs the same trip count (the shuffles need the whole wave)
-    for (int k0 = (tid >> 6) * 2; k0 < nd; k0 += NH) {
-        const int k = k0 + (half & 1);
-        const bool live = k < nd;
-        const int i = live ? list[k] : list[k0];
-        const T *t = feat + (size_t)tex[i] * 3 * cs;
-        const T *rf = fref + (size_t)(p0 + i) * ld;
-        double v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = 0.0;
-        if (vec) gather_half<T, true>(t, rf, cs, cb, ce, l32, v);
-        else gather_half<T, false>(t, rf, cs, cb, ce, l32, v);
-        const double r = reduce8_in32(v, lane);
-        const int e = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
-        if (live && (lane & 3) == 0 && e < 6) rec[(size_t)i * RECW + e] = r;
-    }
-}
-
 // Transposed reduction of 8 values over the 16 lanes of a row (DPP only): halving at
 // bits 3, 2, 1 then a butterfly at bit 0.  Returns the row total of value index
 // 4*b3 + 2*b2 + b1 of l16.
@@ -433,56 +375,32 @@ __device__ __forceinline__ double reduce8_in16(double v[8], int l16) {
 }
 
 // ---------------------------------------------------------------------------
-// B1: rho, rho' per point; team max |rho| for the ratio test.  Returns false on abort.
+// Ratio test (model.py:120-129): the team's max |rho| (order-free: exact) from every
+// wave's maximum.  Returns false on abort.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool phase_loss(int mmax) {
+__device__ __forceinline__ bool ratio_exchange(double lmax) {
     LMState &st = S();
     const Ctx &c = st.c;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int *tex = lds_tex(mmax);
-    double *rec = lds_rec(mmax);
-    const int loss = c.mode == FMPNP_MODE_COMPUTE_COST ? (int)FMPNP_SQUARED : c.loss;
-    double lmax = -1.0;  // -1: nothing supported seen yet
-    if (tid == 0) {
-        st.gathers += st.ndirty;
-        st.ndirty = 0;  // next write: the next projection, several barriers later
-    }
-    for (int i = tid; i < c.M; i += NT) {
-        double rho = 0.0, d1 = 0.0;
-        if (tex[i] >= 0) {
-            loss_eval(loss, c.alpha, 0.5 * rec[(size_t)i * RECW + 0], rho, d1);
-            const double am = fabs(rho);
-            if (isnan(am) || am > lmax) lmax = isnan(lmax) ? lmax : am;
-        }
-        rec[(size_t)i * RECW + 6] = rho;
-        rec[(size_t)i * RECW + 7] = d1;
-    }
-    if (!c.use_ratio) return true;
-    // wave max then workgroup max (max is order-independent: exact)
     lmax = wave_nanmax(lmax);
     if (lane == 0) st.wg_max[wave] = lmax;
     __syncthreads();
     if (tid == 0) {
         double m = st.wg_max[0];
-        for (int w = 1; w < NT / 64; ++w)
-            if (isnan(st.wg_max[w]) || st.wg_max[w] > m) m = isnan(m) ? m : st.wg_max[w];
+        for (int w = 1; w < NT / 64; ++w) m = nanmax(m, st.wg_max[w]);
         st.rho_max = m;
         if (c.G > 1) st_sc1(c.max_g + ((c.epoch + 1) & 1) * c.G + c.s, m);
     }
-    __syncthreads();
     if (c.G > 1) {
-        if (!team_sync()) return false;
-        if (tid == 0) {
+        team_arrive();
+        if (tid < 64 && team_wait() && tid == 0) {
             double m = -1.0;
-            for (int w = 0; w < c.G; ++w) {
-                const double o = ld_sc1(c.max_g + (c.epoch & 1) * c.G + w);
-                if (isnan(o) || o > m) m = isnan(m) ? m : o;
-            }
+            for (int w = 0; w < c.G; ++w) m = nanmax(m, ld_sc1(c.max_g + (c.epoch & 1) * c.G + w));
             st.rho_max = m;
         }
-        __syncthreads();
     }
-    return true;
+    __syncthreads();
+    return !st.abort_flag;
 }
 
 // ---------------------------------------------------------------------------
@@ -497,119 +415,242 @@ __device__ __forceinline__ constexpr int h_col(int k) {
     return k < 6 ? k : k < 11 ? k - 5 : k < 15 ? k - 9 : k < 18 ? k - 12 : k < 20 ? k - 14 : 5;
 }
 
-__device__ __forceinline__ void phase_contrib(int mmax) {
+// One 64-point block of a wave: lane = point.  Points that do not contribute get w = 0
+// and a harmless geometry (z = 1).  Writes the block's four chunk partials.
+__device__ __forceinline__ void contrib_block(int mmax, int blk, bool sup, bool kept, double rho, double d1,
+                                              const double *r, const double Pc[3]) {
     LMState &st = S();
     const Ctx &c = st.c;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = tid & 15;
-    const int *tex = lds_tex(mmax);
-    const double *rec = lds_rec(mmax);
-    const double *Pl = lds_P(mmax);
-    double *part_lds = lds_part(mmax);
-    const double limit = st.rho_max * c.ratio_thr;
-    const bool ratio = c.use_ratio != 0;
+    const int lane = threadIdx.x & 63, l16 = lane & 15;
     const double fx = c.K[0], fy = c.K[4];
-    const int LC = c.LC, M = c.M;
-    double *part_g = c.part_g + (size_t)((c.epoch + 1) & 1) * c.nc_max * NV;
-    for (int base = wave * 4; base < LC; base += 4 * (NT / 64)) {
-        const int lc = base + (lane >> 4);
-        const int i = lc * CH + l16;  // local point index
-        const bool sup = lc < LC && i < M && tex[i] >= 0;
-        const double *r = rec + (size_t)(sup ? i : 0) * RECW;
-        const bool kept = sup && (!ratio || fabs(r[6]) < limit);
-        // points that do not contribute get w = 0 and a harmless geometry (z = 1)
-        const double w = kept ? r[7] : 0.0, rho = kept ? r[6] : 0.0;
-        const double P0 = kept ? Pl[3 * i] : 0.0, P1 = kept ? Pl[3 * i + 1] : 0.0, z = kept ? Pl[3 * i + 2] : 1.0;
-        const double sex = kept ? r[1] : 0.0, sey = kept ? r[2] : 0.0;
-        const double sxx = kept ? r[3] : 0.0, sxy = kept ? r[4] : 0.0, syy = kept ? r[5] : 0.0;
-        // J_px_p (model.py:377-382) times J_p_T (model.py:369-370): A (2x6), A0[1] = A1[0] = 0
-        // one reciprocal instead of six divisions (Jacobian entries only: last-bit level)
-        const double iz = 1.0 / z;
-        const double j00 = fx * iz, j02 = ((-fx) * P0 * iz) * iz;
-        const double j11 = fy * iz, j12 = ((-fy) * P1 * iz) * iz;
-        const double A0[6] = {j00, 0.0, j02, j02 * P1, j00 * z - j02 * P0, -j00 * P1};
-        const double A1[6] = {0.0, j11, j12, -j11 * z + j12 * P1, -j12 * P0, j11 * P0};
-        double M0[6], M1[6];
+    const int lc = blk * 4 + (lane >> 4);
+    const double w = kept ? d1 : 0.0, rh = kept ? rho : 0.0;
+    const double P0 = kept ? Pc[0] : 0.0, P1 = kept ? Pc[1] : 0.0, z = kept ? Pc[2] : 1.0;
+    const double sex = kept ? r[1] : 0.0, sey = kept ? r[2] : 0.0;
+    const double sxx = kept ? r[3] : 0.0, sxy = kept ? r[4] : 0.0, syy = kept ? r[5] : 0.0;
+    // J_px_p (model.py:377-382) times J_p_T (model.py:369-370): A (2x6), A0[1] = A1[0] = 0
+    // one reciprocal instead of six divisions (Jacobian entries only: last-bit level)
+    const double iz = 1.0 / z;
+    const double j00 = fx * iz, j02 = ((-fx) * P0 * iz) * iz;
+    const double j11 = fy * iz, j12 = ((-fy) * P1 * iz) * iz;
+    const double A0[6] = {j00, 0.0, j02, j02 * P1, j00 * z - j02 * P0, -j00 * P1};
+    const double A1[6] = {0.0, j11, j12, -j11 * z + j12 * P1, -j12 * P0, j11 * P0};
+    // w folded into the 2x2 channel moments; the structural zeros A0[1] = A1[0] = 0 are
+    // skipped explicitly (IEEE arithmetic cannot drop 0 * x by itself)
+    const double wxx = w * sxx, wxy = w * sxy, wyy = w * syy, wex = w * sex, wey = w * sey;
+    double M0[6], M1[6];  // (w S) A: M0 = row x, M1 = row y
+    M0[0] = wxx * A0[0];
+    M1[0] = wxy * A0[0];
+    M0[1] = wxy * A1[1];
+    M1[1] = wyy * A1[1];
 #pragma unroll
-        for (int l = 0; l < 6; ++l) {
-            M0[l] = sxx * A0[l] + sxy * A1[l];
-            M1[l] = sxy * A0[l] + syy * A1[l];
+    for (int l = 2; l < 6; ++l) {
+        M0[l] = wxx * A0[l] + wxy * A1[l];
+        M1[l] = wxy * A0[l] + wyy * A1[l];
+    }
+    double *dst_l = lds_part(mmax) + (size_t)(c.c0 + lc) * NV;  // G == 1 (the LDS address space)
+    double *dst_g = c.part_g + (size_t)((c.epoch + 1) & 1) * c.nc_max * NV + (size_t)(c.c0 + lc) * NV;
+    // the 32-value vector in four quarters of 8: only 8 doubles live per reduction
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        double v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int k = 8 * q + e;
+            if (k < 21) {  // H[a][b] = A_a^T (w S) A_b
+                const int a = h_row(k), b = h_col(k);
+                v[e] = a == 0 ? A0[0] * M0[b] : a == 1 ? A1[1] * M1[b] : A0[a] * M0[b] + A1[a] * M1[b];
+            } else if (k < 27) {  // g = A^T (w G^T e)
+                const int l = k - 21;
+                v[e] = l == 0 ? A0[0] * wex : l == 1 ? A1[1] * wey : A0[l] * wex + A1[l] * wey;
+            } else if (k == 27) {
+                v[e] = rh;
+            } else if (k == 28) {
+                v[e] = kept ? 1.0 : 0.0;
+            } else if (k == 29) {
+                v[e] = sup ? 1.0 : 0.0;
+            } else {
+                v[e] = 0.0;
+            }
         }
-        const int chunk = c.c0 + lc;
-        double *dst = c.G == 1 ? part_lds + (size_t)chunk * NV : part_g + (size_t)chunk * NV;
-        // the 32-value vector in four quarters of 8: only 8 doubles live per reduction
+        const double tot = reduce8_in16(v, l16);
+        const int idx = 8 * q + 4 * ((l16 >> 3) & 1) + 2 * ((l16 >> 2) & 1) + ((l16 >> 1) & 1);
+        if (lc < c.LC && (l16 & 1) == 0) {
+            if (c.G == 1) dst_l[idx] = tot;
+            else st_sc1(dst_g + idx, tot);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// One evaluation at (Re, te) over the wave's blocks (no workgroup barrier inside).
+// Without the ratio test each block goes straight on to its chunk partials; with it the
+// loss values are parked in the records and the wave's max |rho| is returned.
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ double eval_pass(int mmax, long long &ngath) {
+    LMState &st = S();
+    const Ctx &c = st.c;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l32 = lane & 31;
+    const bool hi = lane >= 32;
+    const double *X = lds_X(mmax);
+    double *rec = lds_rec(mmax);
+    int *tex = lds_tex(mmax);
+    const T *feat = reinterpret_cast<const T *>(c.feat);
+    const T *fref = reinterpret_cast<const T *>(c.fref);
+    const int cs = c.cs, cb = c.cb, ce = c.ce, p0 = c.p0, ld = c.ld_ref, M = c.M;
+    constexpr int V = V16<T>::n;
+    const bool vec = ((((uintptr_t)feat) | ((uintptr_t)fref)) & 15) == 0 && cs % V == 0 && ld % V == 0 &&
+                     cb % V == 0 && (ce - cb) % V == 0;
+    const int loss = c.mode == FMPNP_MODE_COMPUTE_COST ? (int)FMPNP_SQUARED : c.loss;
+    const bool defer = c.use_ratio != 0;
+    double Re[9], te[3];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+    for (int k = 0; k < 9; ++k) Re[k] = st.Re[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) te[k] = st.te[k];
+    double lmax = -1.0;  // -1: nothing supported seen yet
+    for (int blk = wave; blk * 64 < M; blk += NT / 64) {
+        const int i = blk * 64 + lane;
+        const bool valid = i < M;
+        // projection (model.py:303-311) and indexing_ (model.py:88-89): floor(y*Hf/H),
+        // floor(x*Wf/W) of the reference's fp64 expression equal the integer quotients
+        // (exact products, a correctly rounded quotient of integers floors to the integer
+        // quotient), computed here with invariant-multiplier division
+        double Pc[3] = {0.0, 0.0, 1.0};
+        int off = -1;
+        if (valid) {
+            transform_pt(Re, te, X[3 * i], X[3 * i + 1], X[3 * i + 2], Pc);
+            int x, y;
+            if (project_px(c.K, Pc, c.im_w, c.im_h, x, y)) {
+                const int row = (int)udiv((unsigned)y * (unsigned)c.Hf, c.div_h);
+                const int col = (int)udiv((unsigned)x * (unsigned)c.Wf, c.div_w);
+                off = row * c.Wf + col;
+            }
+        }
+        // memoised gather: a point whose texel did not change keeps its record (the six
+        // channel sums depend only on the texel and the point's fixed descriptor)
+        const int old = valid ? tex[i] : -1;
+        const bool dirty = off >= 0 && (off != old || c.no_memo);
+        if (valid) tex[i] = off;
+        unsigned long long m = __ballot(dirty);
+        ngath += __popcll(m);
+        dbg_stamp(0);
+        while (m) {  // wave-uniform: two dirty points per trip, one per half-wave
+            const int a = __builtin_ctzll(m);
+            m &= m - 1;
+            const bool two = m != 0;
+            const int b = two ? __builtin_ctzll(m) : a;
+            if (two) m &= m - 1;
+            const int oa = __builtin_amdgcn_readlane(off, a), ob = __builtin_amdgcn_readlane(off, b);
+            const int j = hi ? b : a, to = hi ? ob : oa;
+            const int ii = blk * 64 + j;
+            const T *t = feat + (size_t)to * 3 * cs;
+            const T *rf = fref + (size_t)(p0 + ii) * ld;
             double v[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int k = 8 * q + e;
-                if (k < 21) {
-                    const int a = h_row(k), b = h_col(k);
-                    v[e] = w * (A0[a] * M0[b] + A1[a] * M1[b]);
-                } else if (k < 27) {
-                    v[e] = w * (A0[k - 21] * sex + A1[k - 21] * sey);
-                } else if (k == 27) {
-                    v[e] = rho;
-                } else if (k == 28) {
-                    v[e] = kept ? 1.0 : 0.0;
-                } else if (k == 29) {
-                    v[e] = sup ? 1.0 : 0.0;
-                } else {
-                    v[e] = 0.0;
-                }
-            }
-            const double tot = reduce8_in16(v, l16);
-            const int idx = 8 * q + 4 * ((l16 >> 3) & 1) + 2 * ((l16 >> 2) & 1) + ((l16 >> 1) & 1);
-            if (lc < LC && (l16 & 1) == 0) {
-                if (c.G == 1) dst[idx] = tot;
-                else st_sc1(dst + idx, tot);
-            }
-            __builtin_amdgcn_sched_barrier(0);
+            for (int e = 0; e < 8; ++e) v[e] = 0.0;
+            if (vec) gather_half<T, true>(t, rf, cs, cb, ce, l32, v);
+            else gather_half<T, false>(t, rf, cs, cb, ce, l32, v);
+            const double r = reduce8_in32(v, lane);
+            const int e = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
+            if ((lane & 3) == 0 && e < 6 && (!hi || two)) rec[(size_t)ii * RECW + e] = r;
         }
+        // the records just written are read by other lanes of this wave: LDS operations of
+        // a wave complete in order; the clobber keeps the compiler from reordering them
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        dbg_stamp(1);
+        const bool sup = off >= 0;
+        const double *r = rec + (size_t)(valid ? i : 0) * RECW;
+        double rho = 0.0, d1 = 0.0;
+        if (sup) loss_eval(loss, c.alpha, 0.5 * r[0], rho, d1);
+        if (defer) {
+            if (valid) {
+                rec[(size_t)i * RECW + 6] = rho;
+                rec[(size_t)i * RECW + 7] = d1;
+            }
+            if (sup) lmax = nanmax(lmax, fabs(rho));
+        } else {
+            contrib_block(mmax, blk, sup, sup, rho, d1, r, Pc);
+        }
+        dbg_stamp(2);
     }
+    return lmax;
 }
 
-// ---------------------------------------------------------------------------
-// Combine: (G > 1: exchange + stage every chunk partial in LDS), then the ordered sum
-// over chunk indices: tree[q][j] = sum_{c = q, q+NQ, ...} part[c][j] in c order
-// (NQ = NT/32 = 32 rows), then a fixed pairwise tree over the NQ rows.  Depends only on
-// the chunk partials and NC -- not on G, placement or timing.
-// ---------------------------------------------------------------------------
-constexpr int NQ = NT / NV;
-
-__device__ __forceinline__ bool phase_combine(int mmax) {
+// Second pass of the ratio test: the weights of points with |rho| >= max|rho| * thr
+// are zero (model.py:324-336); P is recomputed bit-identically from X.
+__device__ __forceinline__ void contrib_pass(int mmax) {
     LMState &st = S();
     const Ctx &c = st.c;
-    const int tid = threadIdx.x;
-    double *part_lds = lds_part(mmax);
-    const int NC = c.NC;
-    if (c.G > 1) {
-        if (!team_sync()) return false;
-        const double *src = c.part_g + (size_t)(c.epoch & 1) * c.nc_max * NV;
-        for (int e = tid; e < NC * NV; e += NT) part_lds[e] = ld_sc1(src + e);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const double *X = lds_X(mmax);
+    const double *rec = lds_rec(mmax);
+    const int *tex = lds_tex(mmax);
+    const double limit = st.rho_max * c.ratio_thr;
+    double Re[9], te[3];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Re[k] = st.Re[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) te[k] = st.te[k];
+    for (int blk = wave; blk * 64 < c.M; blk += NT / 64) {
+        const int i = blk * 64 + lane;
+        const bool valid = i < c.M;
+        const bool sup = valid && tex[i] >= 0;
+        double Pc[3] = {0.0, 0.0, 1.0};
+        if (sup) transform_pt(Re, te, X[3 * i], X[3 * i + 1], X[3 * i + 2], Pc);
+        const double *r = rec + (size_t)(valid ? i : 0) * RECW;
+        const bool kept = sup && fabs(r[6]) < limit;
+        contrib_block(mmax, blk, sup, kept, r[6], r[7], r, Pc);
     }
-    __syncthreads();
-    {
-        const int j = tid & (NV - 1), q = tid / NV;
-        double acc = 0.0;
-        for (int ch = q; ch < NC; ch += NQ) acc += part_lds[ch * NV + j];
-        st.tree[q][j] = acc;
-    }
-    __syncthreads();
-    return true;
 }
 
-// Final level of the ordered sum on wave 0 (no barrier: the LM update that reads the
-// totals runs on the same wave): lane l sums rows 16*(l>>5) .. +15 of value l&31 with a
-// fixed pairwise tree, the two halves are added across the wave -- the same tree as a
-// single pairwise tree over the NQ = 32 rows.
-static_assert(NQ == 32, "final tree assumes 32 rows");
-__device__ __forceinline__ void combine_final_wave() {
+// ---------------------------------------------------------------------------
+// Combine on wave 0 (after the barrier / team exchange): the ordered sum over chunk
+// indices.  Row q of NQ = 32 rows sums chunks q, q+32, ... in chunk order; a fixed
+// pairwise tree over the rows follows (lane l: value l&31, rows 16*(l>>5) .. +15; the
+// halves are added across the wave).  Depends only on the chunk partials and NC -- not
+// on G, placement or timing.
+// ---------------------------------------------------------------------------
+constexpr int NQ = 32;
+
+__device__ __forceinline__ void combine_final_wave(int mmax) {
     LMState &st = S();
+    const Ctx &c = st.c;
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    const int NC = c.NC;
     double t[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) t[q] = st.tree[16 * h + q][j];
+    for (int q = 0; q < 16; ++q) t[q] = 0.0;
+    // rounds of 32 chunks: the 16 loads of a round are issued before their adds; per row
+    // the adds stay in chunk order
+    if (c.G == 1) {
+        const double *src = lds_part(mmax);
+        for (int r0 = 0; r0 < NC; r0 += NQ) {
+            double v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int ch = r0 + 16 * h + q;
+                v[q] = ch < NC ? src[ch * NV + j] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if (r0 + 16 * h + q < NC) t[q] += v[q];
+        }
+    } else {
+        const double *src = c.part_g + (size_t)(c.epoch & 1) * c.nc_max * NV;
+        for (int r0 = 0; r0 < NC; r0 += NQ) {
+            double v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int ch = r0 + 16 * h + q;
+                v[q] = ch < NC ? ld_sc1(src + ch * NV + j) : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if (r0 + 16 * h + q < NC) t[q] += v[q];
+        }
+    }
 #pragma unroll
     for (int w = 1; w < 16; w *= 2)
 #pragma unroll
@@ -618,8 +659,7 @@ __device__ __forceinline__ void combine_final_wave() {
     swap32(a, b);  // low half: (own, partner); high half: (partner, own)
     const double tot = a + b;  // rows 0..15 + rows 16..31 in both halves
     if (lane < NV) st.tot[lane] = tot;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back by this wave only
 }
 
 // ---------------------------------------------------------------------------
@@ -919,46 +959,41 @@ __global__ __launch_bounds__(NT, FMPNP_LM_WAVES_PER_SIMD) void lm_kernel(LaunchA
         c.dead = 0;
     }
     __syncthreads();
-    // optional phase stamps (debug: a.stamps != null): s_memtime deltas on lane 0 after barriers
+    // optional phase stamps (debug: a.stamps != null): s_memtime deltas on thread 0
     const bool stamps_on = a.stamps != nullptr;
     if (stamps_on && tid == 0) {
         for (int k = 0; k < NSTAMP; ++k) st.stamp_ph[k] = 0;
         st.stamp_t = __builtin_amdgcn_s_memtime();
     }
-#define STAMP(k)                                                \
-    if (stamps_on && tid == 0) {                                \
-        unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
-        st.stamp_ph[(k) < 4 && st.n_evals == 0 ? 8 + (k) : (k)] += now_ - st.stamp_t; \
-        st.stamp_t = now_;                                      \
-    }
-
     for (int p = team; p < a.n; p += a.teams) {
         problem_begin(a.probs + p, p, mmax);
+        long long ngath = 0;  // texel gathers of this wave for this problem
         while (!st.done) {
-            phase_project(mmax);
-            __syncthreads();
-            STAMP(0);
-            phase_gather<T>(mmax);
-            __syncthreads();
-            STAMP(1);
-            if (!phase_loss(mmax)) break;
-            STAMP(2);
-            phase_contrib(mmax);
-            STAMP(3);
-            if (!phase_combine(mmax)) break;
-            if (tid < 64) {
-                combine_final_wave();
-                STAMP(4);
+            const double lmax = eval_pass<T>(mmax, ngath);  // project, gather, loss (+ partials)
+            if (st.c.use_ratio) {
+                if (!ratio_exchange(lmax)) break;
+                contrib_pass(mmax);
+            }
+            if (st.c.G > 1) team_arrive();
+            else __syncthreads();
+            if (tid < 64 && (st.c.G == 1 || team_wait())) {
+                dbg_stamp(3);  // slowest wave + exchange
+                combine_final_wave(mmax);
+                dbg_stamp(4);
                 lm_update_wave();
             }
             __syncthreads();
-            STAMP(7);  // pose update + barrier
+            dbg_stamp(7);  // pose update + barrier
+            if (st.abort_flag) break;
         }
+        // every wave of every team member adds its share (results are zeroed by the launcher)
+        if ((tid & 63) == 0 && ngath)
+            atomicAdd(reinterpret_cast<unsigned long long *>(&a.results[p].texel_gathers),
+                      (unsigned long long)ngath);
         problem_end();
     }
     if (stamps_on && tid == 0)
         for (int k = 0; k < NSTAMP; ++k) a.stamps[(size_t)blockIdx.x * NSTAMP + k] = st.stamp_ph[k];
-#undef STAMP
 }
 
 template __global__ void lm_kernel<float>(LaunchArgs);
@@ -975,8 +1010,8 @@ const void *lm_kernel_ptr(int dtype) {
 }
 
 size_t lm_dyn_lds_bytes(int mmax, int nc_max) {
-    // X[3M] + P[3M] + rec[RECW M] doubles, tex[M] + list[M] ints (+16 B pad), part[nc_max][NV] doubles
-    return (size_t)(6 + RECW) * mmax * 8 + ((size_t)mmax + 2) * 8 + (size_t)nc_max * NV * 8;
+    // X[3M] + rec[RECW M] doubles, tex[M] ints (16-B padded), part[nc_max][NV] doubles
+    return (size_t)(3 + RECW) * mmax * 8 + (size_t)((mmax + 3) / 4) * 16 + (size_t)nc_max * NV * 8;
 }
 
 }  // namespace fmpnp

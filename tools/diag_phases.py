@@ -34,8 +34,8 @@ res = ab.results()
 g = sum(r["texel_gathers"] for r in res)
 full = sum(r["n_evals"] for r in res) * 512
 print(f"texel gathers {g} of {full} point-evals ({100.0 * g / max(full, 1):.1f} %)")
-names = ["A0 proj", "A gather", "B1 loss", "B2 contrib", "combine", "LM state", "LU solve", "pose+sync",
-         "eval0 proj", "eval0 gather", "eval0 loss", "eval0 contrib"]
+names = ["proj (w0)", "gather (w0)", "loss+contrib", "wait/exchange", "combine", "LM state", "solve",
+         "pose+sync", "eval0 proj", "eval0 gather", "eval0 l+c", "eval0 wait"]
 tot = ph.sum(0)
 print(f"B={B} launch={info} stamped launch {e0.elapsed_time(e1):.3f} ms, plain launch median {np.median(plain):.3f} ms (min {min(plain):.3f}) -> {B / np.median(plain) * 1e3:.0f} /s")
 for k in range(12):
