@@ -118,7 +118,8 @@ __device__ __forceinline__ void pose_update(const double *R, const double *t, co
 #pragma unroll
         for (int i = 0; i < 9; ++i) dR[i] = NAN;
     } else if (!(theta < 1e-12)) {
-        const double k0 = w0 / theta, k1 = w1 / theta, k2 = w2 / theta;
+        const double it = 1.0 / theta;  // w / theta within 1 ulp, one division instead of three
+        const double k0 = w0 * it, k1 = w1 * it, k2 = w2 * it;
         const double W[9] = {0, -k2, k1, k2, 0, -k0, -k1, k0, 0};
         double s, c;
         sincos(theta, &s, &c);
@@ -765,7 +766,10 @@ __device__ __forceinline__ bool ldlt_step(const double *Hu, const double *g, dou
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
         ok &= a[j][j] > 0.0;  // false for NaN
-        inv[j] = 1.0 / a[j][j];
+        // reciprocal by v_rcp_f64 + one Newton step (~1 ulp; the solve is not bit-pinned to
+        // the reference's LU anyway) instead of a full IEEE division on the critical path
+        const double r0 = __builtin_amdgcn_rcp(a[j][j]);
+        inv[j] = fma(fma(-a[j][j], r0, 1.0), r0, r0);
         double u[6];
 #pragma unroll
         for (int i = j + 1; i < 6; ++i) u[i] = a[i][j];
