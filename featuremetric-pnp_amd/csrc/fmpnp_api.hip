@@ -21,7 +21,7 @@ namespace {
 
 struct Plan {
     int G = 1, teams = 1, teams_pad = 8, gw = 8, grid = 8, nc_max = 1, max_n = 0;
-    int mmax = 0, lds = 0;
+    int mmax = 0, lds = 0, wps = WPS_LATENCY;
     size_t ws_counters = 0, ws_partials = 0, ws_max = 0, ws_total = 0;
 };
 
@@ -81,7 +81,8 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     // (MI355X_MICROARCH.md, Residency) -> min(api, 6).
     auto occupancy = [&](int lds) {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lm_kernel_ptr(opt->dtype), NT, lds) != hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lm_kernel_ptr(opt->dtype, P.wps), NT, lds) !=
+            hipSuccess)
             return 1;
         return std::max(1, std::min(nb, 6));
     };
@@ -94,7 +95,8 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     if (opt->wgs_per_problem > 0) {
         G = std::min(opt->wgs_per_problem, P.nc_max);
     } else {
-        G = (n <= 0 || 2L * n >= ncu) ? 1 : (ncu + n - 1) / n;
+        // (no_memo re-reads every texel: bandwidth-bound, so every CU gets a workgroup)
+        G = (n <= 0 || (2L * n >= ncu && !opt->no_memo)) ? 1 : (ncu + n - 1) / n;
         G = std::max(1, std::min(G, P.nc_max));
     }
     G = std::min(G, MAX_G);
@@ -103,6 +105,9 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     P.G = G;
     P.mmax = ((P.nc_max + G - 1) / G) * CH;
     P.lds = lds_for(G);
+    // two workgroups per CU once there are enough single-workgroup problems to fill them
+    // (measured B=512: 1.11 -> 0.99 ms); below that the 256-VGPR variant is faster
+    P.wps = (G == 1 && (long)n >= 2L * ncu && 2 * P.lds <= lds_cu) ? WPS_THROUGHPUT : WPS_LATENCY;
     const int per_cu = occupancy(P.lds);
     long cap = (long)ncu * per_cu;
     if (G == 1) cap = std::max(cap, (long)n);  // no cross-workgroup waits: any grid is safe
@@ -220,6 +225,7 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
     a.maxslots = (double *)(ws + P.ws_counters + P.ws_partials);
     a.mmax = P.mmax;
     a.stamps = g_stamps;
+    a.wps = P.wps;
     hipError_t e = hipMemsetAsync(a.counters, 0, P.ws_counters, s);
     if (e != hipSuccess) return (int)e;
     e = hipMemsetAsync(results_dev, 0, sizeof(fmpnp_result) * (size_t)n, s);  // texel_gathers accumulate

@@ -13,9 +13,10 @@ constexpr int NV = 32;          // reduced vector: 21 H + 6 g + rho + kept + sup
 constexpr int NSTAMP = 12;      // debug phase-stamp slots: 8 phases + eval-0 proj/gather/loss/contrib
 constexpr int RECW = 8;         // per-point record: 6 channel sums + rho + rho'
 constexpr int MAX_G = 64;       // workgroups per problem
-#ifndef FMPNP_LM_WAVES_PER_SIMD
-#define FMPNP_LM_WAVES_PER_SIMD 2   // LM kernel occupancy target: one 512-thread workgroup per CU, <= 256 VGPRs
-#endif
+// LM kernel occupancy variants (waves per SIMD in __launch_bounds__): 2 = one 512-thread
+// workgroup per CU with up to 256 VGPRs (latency); 4 = two per CU within 128 VGPRs, so one
+// problem's serial LM tail overlaps another's point work (throughput, batches >= 2 x CUs)
+constexpr int WPS_LATENCY = 2, WPS_THROUGHPUT = 4;
 
 // Kernel arguments (by value).
 struct LaunchArgs {
@@ -31,6 +32,7 @@ struct LaunchArgs {
     double *maxslots;             // [teams][2][G]
     int mmax;                     // max points per workgroup (multiple of CH): dynamic LDS carve
     unsigned long long *stamps;   // debug: [grid][NSTAMP] phase cycle totals, or null
+    int wps;                      // occupancy variant (WPS_LATENCY / WPS_THROUGHPUT)
 };
 
 // Fixed LDS head: the LM state + per-problem context (sized generously, 16-B aligned).
@@ -38,7 +40,7 @@ __host__ __device__ constexpr int lds_fixed_bytes() { return 4096; }
 size_t lm_dyn_lds_bytes(int mmax, int nc_max);
 
 hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream);
-const void *lm_kernel_ptr(int dtype);
+const void *lm_kernel_ptr(int dtype, int wps);
 
 hipError_t launch_pack(const void *chw, const void *gx, const void *gy, int dtype_in, int C, int H, int W, void *out,
                        int dtype_out, int cstride, int normalized, int replicate, hipStream_t stream);

@@ -926,8 +926,8 @@ __device__ __forceinline__ void lm_update_wave() {
 // ---------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(NT, FMPNP_LM_WAVES_PER_SIMD) void lm_kernel(LaunchArgs a) {
+template <typename T, int WPS>
+__global__ __launch_bounds__(NT, WPS) void lm_kernel(LaunchArgs a) {
     LMState &st = S();
     const int G = a.G;
     // XCD-aware team placement: members of one team share blockIdx % gw (the same XCD
@@ -1000,17 +1000,24 @@ __global__ __launch_bounds__(NT, FMPNP_LM_WAVES_PER_SIMD) void lm_kernel(LaunchA
         for (int k = 0; k < NSTAMP; ++k) a.stamps[(size_t)blockIdx.x * NSTAMP + k] = st.stamp_ph[k];
 }
 
-template __global__ void lm_kernel<float>(LaunchArgs);
-template __global__ void lm_kernel<double>(LaunchArgs);
+template __global__ void lm_kernel<float, WPS_LATENCY>(LaunchArgs);
+template __global__ void lm_kernel<double, WPS_LATENCY>(LaunchArgs);
+template __global__ void lm_kernel<float, WPS_THROUGHPUT>(LaunchArgs);
+template __global__ void lm_kernel<double, WPS_THROUGHPUT>(LaunchArgs);
 
 hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream) {
-    if (dtype == FMPNP_F32) hipLaunchKernelGGL((lm_kernel<float>), dim3(grid), dim3(NT), lds, stream, a);
-    else hipLaunchKernelGGL((lm_kernel<double>), dim3(grid), dim3(NT), lds, stream, a);
+    const bool f32 = dtype == FMPNP_F32, tp = a.wps == WPS_THROUGHPUT;
+    if (f32 && !tp) hipLaunchKernelGGL((lm_kernel<float, WPS_LATENCY>), dim3(grid), dim3(NT), lds, stream, a);
+    else if (f32) hipLaunchKernelGGL((lm_kernel<float, WPS_THROUGHPUT>), dim3(grid), dim3(NT), lds, stream, a);
+    else if (!tp) hipLaunchKernelGGL((lm_kernel<double, WPS_LATENCY>), dim3(grid), dim3(NT), lds, stream, a);
+    else hipLaunchKernelGGL((lm_kernel<double, WPS_THROUGHPUT>), dim3(grid), dim3(NT), lds, stream, a);
     return hipGetLastError();
 }
 
-const void *lm_kernel_ptr(int dtype) {
-    return dtype == FMPNP_F32 ? (const void *)lm_kernel<float> : (const void *)lm_kernel<double>;
+const void *lm_kernel_ptr(int dtype, int wps) {
+    const bool f32 = dtype == FMPNP_F32, tp = wps == WPS_THROUGHPUT;
+    if (f32) return tp ? (const void *)lm_kernel<float, WPS_THROUGHPUT> : (const void *)lm_kernel<float, WPS_LATENCY>;
+    return tp ? (const void *)lm_kernel<double, WPS_THROUGHPUT> : (const void *)lm_kernel<double, WPS_LATENCY>;
 }
 
 size_t lm_dyn_lds_bytes(int mmax, int nc_max) {

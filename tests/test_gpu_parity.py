@@ -138,6 +138,30 @@ def test_batch_equals_individual():
         assert r1["status"] == rb["status"]
 
 
+def test_large_batch_throughput_variant_equals_individual():
+    """n >= 2 x CUs selects the two-workgroups-per-CU kernel (128 VGPRs): its results must be
+    bit-identical to single-problem launches (which use the 256-VGPR kernel)."""
+    names = ["gm_c16", "behind_camera_gm", "odd_geom_gm", "no_support_init", "ratio08_gm"]
+    base = []
+    for nm in names:
+        inp, meta, gold = case(nm)
+        f, gx, gy = maps64(inp, orc.sobel)
+        feats = rf.pack_features(torch.from_numpy(f), torch.from_numpy(gx), torch.from_numpy(gy),
+                                 storage=torch.float32, device=DEV)
+        base.append(rf.make_problem(feats, torch.from_numpy(inp["fref"]), inp["pts3d"], inp["K"], inp["im_width"],
+                                    inp["im_height"], inp["R0"], inp["t0"]))
+    n = 2 * torch.cuda.get_device_properties(0).multi_processor_count + 3
+    probs = [base[i % len(base)] for i in range(n)]
+    opts = rf.make_options(20, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32)
+    batch, _ = rf.refine(probs, opts)
+    assert _lib.last_launch()["grid"] >= n
+    singles = [rf.refine([p], opts)[0][0] for p in base]
+    for i, rb in enumerate(batch):
+        r1 = singles[i % len(base)]
+        assert np.array_equal(r1["R"], rb["R"]) and np.array_equal(r1["t"], rb["t"]), i
+        assert r1["status"] == rb["status"] and r1["n_evals"] == rb["n_evals"]
+
+
 def test_pack_sobel_matches_oracle():
     z = load_npz("sobel_small")
     x = z["x"]
