@@ -60,11 +60,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    # one process per GPU; FMPNP_BENCH_BACKEND=gloo (and more ranks than GPUs) rehearses the
+    # distributed path on a one-GPU box -- the timing barrier and max-over-ranks only
+    backend = os.environ.get("FMPNP_BENCH_BACKEND", "nccl")
+    ndev = max(1, torch.cuda.device_count())
+    gpu = local % ndev
     if dist:
         import torch.distributed as tdist
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            tdist.init_process_group(backend)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
 
     import fmpnp
     from fmpnp import _lib, refine as rf, synth
@@ -113,7 +121,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
     res = batch.results()
