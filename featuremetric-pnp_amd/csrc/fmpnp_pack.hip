@@ -8,13 +8,12 @@
 // [H][W][3][C] (f, gx, gy interleaved per texel), so the LM kernel's gather of a
 // point is three contiguous C-long runs.
 //
-// Tiling: a workgroup owns 64 channels x 64 columns x RS rows.  It keeps a ring
-// of three input rows in LDS (row stride 67 elements: conflict-free column
-// reads), loads row y+1 while computing row y, and writes the three output planes
-// with lanes along channels (256-B coalesced stores).  Input is read (RS+2)/RS
-// times, output written once: ~16.5 B of HBM traffic per fp32 element vs 16 ideal.
+// Two kernels: sobel_pack_kernel (gradients computed here; the performance path, see its
+// comment below) and pack_kernel<GIVEN=true> (gradients supplied by the caller, as
+// forward() receives them -- parity runs only).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "fmpnp.h"
 #include "fmpnp_internal.h"
@@ -112,19 +111,248 @@ __global__ __launch_bounds__(PK_NT) void pack_kernel(const Tin *__restrict__ chw
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// sobel_pack_kernel: the Sobel path (gradients computed here), tuned for the HBM roofline.
+//
+// Tile: SB_CB channels x SB_XW columns x `rs` rows (host-chosen so that the grid is about one
+// resident wave of workgroups: 4 per CU).  Input rows stream through a 4-slot LDS ring
+// [slot][SB_CB][SB_LD] (odd row stride: the channel-per-lane reads and the 4-column
+// transposing writes are both bank-conflict free); row y+3's global loads (16-byte vectors
+// along x, 8 lanes per 128-B channel row) are in flight while row y is computed, so one
+// barrier per row and no exposed load latency.  Compute: lane = channel, wave = a run of 8
+// columns, a 3x3 register window slides along x (3 LDS reads per output texel), and each
+// plane store is 64 consecutive channels = 256 contiguous bytes per wave instruction.
+// HBM traffic per texel: 4C * (rs+2)/rs read + 12C written.
+constexpr int SB_NT = 256;
+constexpr int SB_CB = 64;                 // channels per tile (one per lane)
+constexpr int SB_XW = 32;                 // columns per tile (4 waves x 8-column runs)
+constexpr int SB_RUN = SB_XW / (SB_NT / 64);
+constexpr int SB_LD = SB_XW + 5;          // 37: odd, >= XW + 2 halo columns
+constexpr int SB_SLOTS = 4;
+
+template <typename Tin>
+struct SbRow {
+    static constexpr int VE = 16 / sizeof(Tin);                 // elements per 16-B vector
+    static constexpr int QPC = SB_XW / VE;                      // vectors per channel row
+    static constexpr int UNITS = SB_CB * QPC / SB_NT;           // vectors per thread
+    Tin v[UNITS][VE];
+    Tin halo;
+};
+
+template <typename Tin, bool FAST>
+__device__ __forceinline__ void sb_load(SbRow<Tin> &r, const Tin *__restrict__ src, int C, int H, int W, int c0,
+                                        int x0, int y, int replicate) {
+    using R = SbRow<Tin>;
+    const int t = threadIdx.x;
+    int yy = y;
+    bool row_ok = (y >= 0 && y < H);
+    if (!row_ok && replicate) { yy = y < 0 ? 0 : H - 1; row_ok = true; }
+#pragma unroll
+    for (int i = 0; i < R::UNITS; ++i) {
+        const int u = t + SB_NT * i, cc = u / R::QPC, q = u - cc * R::QPC;
+        const int c = c0 + cc, xb = x0 + q * R::VE;
+        const Tin *p = src + ((size_t)c * H + yy) * W + xb;
+        if (FAST && c < C && row_ok) {
+            if constexpr (sizeof(Tin) == 4) {
+                float4 w = *reinterpret_cast<const float4 *>(p);
+                r.v[i][0] = w.x; r.v[i][1] = w.y; r.v[i][2] = w.z; r.v[i][3] = w.w;
+            } else {
+                double2 w = *reinterpret_cast<const double2 *>(p);
+                r.v[i][0] = w.x; r.v[i][1] = w.y;
+            }
+        } else if (!FAST) {
+#pragma unroll
+            for (int k = 0; k < R::VE; ++k) {
+                int x = xb + k;
+                Tin val = 0;
+                if (c < C && row_ok) {
+                    if (x < W) val = p[k];
+                    else if (replicate) val = src[((size_t)c * H + yy) * W + (W - 1)];
+                }
+                r.v[i][k] = val;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < R::VE; ++k) r.v[i][k] = 0;
+        }
+    }
+    r.halo = 0;
+    if (t < 2 * SB_CB) {
+        const int cc = t >> 1, c = c0 + cc;
+        int x = (t & 1) ? x0 + SB_XW : x0 - 1;
+        bool ok = (x >= 0 && x < W);
+        if (!ok && replicate) { x = x < 0 ? 0 : W - 1; ok = true; }
+        if (c < C && row_ok && ok) r.halo = src[((size_t)c * H + yy) * W + x];
+    }
+}
+
+template <typename Tin>
+__device__ __forceinline__ void sb_store(const SbRow<Tin> &r, Tin *slot) {
+    using R = SbRow<Tin>;
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < R::UNITS; ++i) {
+        const int u = t + SB_NT * i, cc = u / R::QPC, q = u - cc * R::QPC;
+#pragma unroll
+        for (int k = 0; k < R::VE; ++k) slot[cc * SB_LD + 1 + q * R::VE + k] = r.v[i][k];
+    }
+    if (t < 2 * SB_CB) slot[(t >> 1) * SB_LD + ((t & 1) ? SB_XW + 1 : 0)] = r.halo;
+}
+
+// Store one output element through the row-tile buffer descriptor: voffset is the lane's
+// channel offset (fixed per row), soffset the texel/plane offset (wave-uniform SGPR).
+template <typename Tout, bool NTS>
+__device__ __forceinline__ void sb_put(Tout v, __amdgpu_buffer_rsrc_t rsrc, int voff, int soff) {
+    constexpr int aux = NTS ? 2 : 0;  // nt: streamed once, do not keep in L2
+    if constexpr (sizeof(Tout) == 4)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rsrc, voff, soff, aux);
+    else
+        {
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rsrc, voff, soff, aux);
+    }
+}
+
+// FULL: the tile's 32 columns are all inside the map (no per-column bound check).
+// NORM: kornia normalized=True (x 1/8).  Arithmetic is fp64 (fp32 maps: exact), rounded once.
+//   Tin = float : separable form, column sums then differences (6 fp64 ops per texel); exact
+//                 in fp64 for fp32 inputs, so the rounded result is the oracle's.
+//   Tin = double: the oracle's association (helpers/sobel_pytorch.py:9-59 order), bit-equal.
+template <typename Tin, typename Tout, bool FULL, bool NORM, bool NTS>
+__device__ __forceinline__ void sb_row(const Tin *rm, const Tin *r0, const Tin *rp, __amdgpu_buffer_rsrc_t rsrc,
+                                       int voff, int soff0, int tstride, int pstride, int ncols) {
+    constexpr double sc = NORM ? 0.125 : 1.0;
+    if constexpr (sizeof(Tin) == 4) {
+        // column j: sx_j = a_j + 2 d_j + g_j (for gx), sy_j = g_j - a_j (for gy)
+        double am = rm[0], dm = r0[0], gm = rp[0];
+        double a1 = rm[1], d1 = r0[1], g1 = rp[1];
+        double sxm = (am + 2.0 * dm) + gm, sym = gm - am;
+        double sx0 = (a1 + 2.0 * d1) + g1, sy0 = g1 - a1;
+        double f0 = d1;
+#pragma unroll
+        for (int k = 0; k < SB_RUN; ++k) {
+            const double a2 = rm[k + 2], d2 = r0[k + 2], g2 = rp[k + 2];
+            const double sxp = (a2 + 2.0 * d2) + g2, syp = g2 - a2;
+            const double gx = sxp - sxm, gy = (sym + 2.0 * sy0) + syp;
+            if (FULL || k < ncols) {
+                const int so = soff0 + k * tstride;
+                sb_put<Tout, NTS>((Tout)f0, rsrc, voff, so);
+                sb_put<Tout, NTS>((Tout)(NORM ? gx * sc : gx), rsrc, voff, so + pstride);
+                sb_put<Tout, NTS>((Tout)(NORM ? gy * sc : gy), rsrc, voff, so + 2 * pstride);
+            }
+            sxm = sx0; sym = sy0; sx0 = sxp; sy0 = syp; f0 = d2;
+        }
+    } else {
+        double a0 = rm[0], a1 = rm[1], d0 = r0[0], d1 = r0[1], g0 = rp[0], g1 = rp[1];
+#pragma unroll
+        for (int k = 0; k < SB_RUN; ++k) {
+            const double a2 = rm[k + 2], d2 = r0[k + 2], g2 = rp[k + 2];
+            // cross-correlation with kx = [[-1,0,1],[-2,0,2],[-1,0,1]], ky = kx^T, oracle order
+            const double gx = ((-a0 + a2) + (-2.0 * d0 + 2.0 * d2)) + (-g0 + g2);
+            const double gy = ((-a0 - 2.0 * a1) - a2) + ((g0 + 2.0 * g1) + g2);
+            if (FULL || k < ncols) {
+                const int so = soff0 + k * tstride;
+                sb_put<Tout, NTS>((Tout)d1, rsrc, voff, so);
+                sb_put<Tout, NTS>((Tout)(NORM ? gx * sc : gx), rsrc, voff, so + pstride);
+                sb_put<Tout, NTS>((Tout)(NORM ? gy * sc : gy), rsrc, voff, so + 2 * pstride);
+            }
+            a0 = a1; a1 = a2; d0 = d1; d1 = d2; g0 = g1; g1 = g2;
+        }
+    }
+}
+
+// FAST: 16-B vector loads (aligned rows) and all 32 tile columns inside the map.
+template <typename Tin, typename Tout, bool NORM, bool NTS, bool FAST>
+__device__ __forceinline__ void sobel_pack_body(const Tin *__restrict__ chw, int C, int H, int W, int cs, int rs,
+                                                int replicate, Tin *ring, __amdgpu_buffer_rsrc_t rsrc) {
+    constexpr int SE = SB_CB * SB_LD;
+    const int c0 = blockIdx.x * SB_CB, x0 = blockIdx.y * SB_XW, y0 = blockIdx.z * rs;
+    const int y1 = min(y0 + rs, H);
+    const int cc = threadIdx.x & 63, run = threadIdx.x >> 6;
+    const int c = c0 + cc;
+    const int wrun = __builtin_amdgcn_readfirstlane(run);  // wave-uniform: store offsets stay in SGPRs
+    const int voff = (c < C ? c : 0) * (int)sizeof(Tout);
+    const int tstride = 3 * cs * (int)sizeof(Tout), pstride = cs * (int)sizeof(Tout);
+    const int ncols = W - (x0 + wrun * SB_RUN);
+
+    SbRow<Tin> r;
+    sb_load<Tin, FAST>(r, chw, C, H, W, c0, x0, y0 - 1, replicate);
+    sb_store<Tin>(r, ring + ((y0 - 1) & 3) * SE);
+    sb_load<Tin, FAST>(r, chw, C, H, W, c0, x0, y0, replicate);
+    sb_store<Tin>(r, ring + (y0 & 3) * SE);
+    sb_load<Tin, FAST>(r, chw, C, H, W, c0, x0, y0 + 1, replicate);
+    sb_store<Tin>(r, ring + ((y0 + 1) & 3) * SE);
+    if (y0 + 2 <= y1) sb_load<Tin, FAST>(r, chw, C, H, W, c0, x0, y0 + 2, replicate);
+    for (int y = y0; y < y1; ++y) {
+        __syncthreads();  // rows y-1, y, y+1 in their slots; nobody reads slot (y+2)&3 any more
+        if (c < C) {
+            const int lo = cc * SB_LD + run * SB_RUN;
+            const Tin *rm = ring + ((y - 1) & 3) * SE + lo;
+            const Tin *r0 = ring + (y & 3) * SE + lo;
+            const Tin *rp = ring + ((y + 1) & 3) * SE + lo;
+            const int soff0 = ((y - y0) * W + x0 + wrun * SB_RUN) * tstride;
+            sb_row<Tin, Tout, FAST, NORM, NTS>(rm, r0, rp, rsrc, voff, soff0, tstride, pstride, ncols);
+        }
+        if (y + 2 <= y1) {
+            sb_store<Tin>(r, ring + ((y + 2) & 3) * SE);
+            if (y + 3 <= y1) sb_load<Tin, FAST>(r, chw, C, H, W, c0, x0, y + 3, replicate);
+        }
+    }
+}
+
+template <typename Tin, typename Tout, bool NORM, bool NTS>
+__global__ __launch_bounds__(SB_NT) void sobel_pack_kernel(const Tin *__restrict__ chw, int C, int H, int W,
+                                                        Tout *__restrict__ out, int cs, int rs, int replicate,
+                                                        int vec_ok) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    Tin *ring = reinterpret_cast<Tin *>(smem);  // [SB_SLOTS][SB_CB][SB_LD]
+    const int x0 = blockIdx.y * SB_XW, y0 = blockIdx.z * rs;
+    const int y1 = min(y0 + rs, H);
+    // descriptor over this tile's output rows [y0, y1) x all columns (byte offsets < 2^31)
+    const size_t texel_elems = (size_t)3 * cs;
+    Tout *tile_base = out + (size_t)y0 * W * texel_elems;
+    const unsigned tile_bytes = (unsigned)((size_t)(y1 - y0) * W * texel_elems * sizeof(Tout));
+    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_base, 0, tile_bytes, 0x00020000);
+    if (vec_ok && x0 + SB_XW <= W)
+        sobel_pack_body<Tin, Tout, NORM, NTS, true>(chw, C, H, W, cs, rs, replicate, ring, rsrc);
+    else
+        sobel_pack_body<Tin, Tout, NORM, NTS, false>(chw, C, H, W, cs, rs, replicate, ring, rsrc);
+}
+
 template <typename Tin, typename Tout>
 static hipError_t pack_t(const void *chw, const void *gx, const void *gy, int C, int H, int W, void *out, int cs,
                          int normalized, int replicate, hipStream_t stream) {
-    dim3 grid((C + PK_CB - 1) / PK_CB, (W + PK_XW - 1) / PK_XW, (H + PK_RS - 1) / PK_RS);
-    size_t lds = 3 * PK_CB * PK_LD * sizeof(Tin);
     if (gx) {
+        dim3 grid((C + PK_CB - 1) / PK_CB, (W + PK_XW - 1) / PK_XW, (H + PK_RS - 1) / PK_RS);
+        size_t lds = 3 * PK_CB * PK_LD * sizeof(Tin);
         hipLaunchKernelGGL((pack_kernel<Tin, Tout, true>), grid, dim3(PK_NT), lds, stream, (const Tin *)chw,
                            (const Tin *)gx, (const Tin *)gy, C, H, W, (Tout *)out, cs, normalized, replicate);
-    } else {
-        hipLaunchKernelGGL((pack_kernel<Tin, Tout, false>), grid, dim3(PK_NT), lds, stream, (const Tin *)chw,
-                           (const Tin *)nullptr, (const Tin *)nullptr, C, H, W, (Tout *)out, cs, normalized,
-                           replicate);
+        return hipGetLastError();
     }
+    // rows per workgroup: about one resident wave of workgroups (4 per CU on 256 CUs), >= 4 rows
+    const int ncb = (C + SB_CB - 1) / SB_CB, nxw = (W + SB_XW - 1) / SB_XW;
+    int nyb = 1024 / (ncb * nxw);
+    if (nyb < 1) nyb = 1;
+    int rs = (H + nyb - 1) / nyb;
+    if (rs < 4) rs = 4;
+    nyb = (H + rs - 1) / rs;
+    const int vec_ok = ((uintptr_t)chw % 16 == 0) && ((size_t)W * sizeof(Tin)) % 16 == 0;
+    dim3 grid(ncb, nxw, nyb);
+    size_t lds = (size_t)SB_SLOTS * SB_CB * SB_LD * sizeof(Tin);
+    // the output descriptor of a workgroup spans its rs rows: byte offsets must stay below 2^31
+    if ((size_t)rs * W * 3 * cs * sizeof(Tout) >= ((size_t)1 << 31)) return hipErrorInvalidValue;
+    // nt stores by default (the packed map is streamed out once; measured 2-17 % faster than
+    // plain stores over cfg2..cfg5 shapes); FMPNP_PACK_NT=0 selects plain stores
+    static const int nts = [] { const char *e = getenv("FMPNP_PACK_NT"); return !(e && *e == '0'); }();
+#define SB_LAUNCH(NORM, NTS)                                                                                    \
+    hipLaunchKernelGGL((sobel_pack_kernel<Tin, Tout, NORM, NTS>), grid, dim3(SB_NT), lds, stream,              \
+                       (const Tin *)chw, C, H, W, (Tout *)out, cs, rs, replicate, vec_ok)
+    if (normalized) {
+        if (nts) SB_LAUNCH(true, true); else SB_LAUNCH(true, false);
+    } else {
+        if (nts) SB_LAUNCH(false, true); else SB_LAUNCH(false, false);
+    }
+#undef SB_LAUNCH
     return hipGetLastError();
 }
 

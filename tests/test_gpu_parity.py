@@ -194,6 +194,43 @@ def test_pack_large_tiles_and_ragged_edges():
     assert not buf[:, :, :, 70:].any()
 
 
+def _sobel_np(x, normalized, replicate):
+    """3x3 Sobel cross-correlation (helpers/sobel_pytorch.py:9-59) with zero or edge padding."""
+    xp = np.pad(x, ((0, 0), (1, 1), (1, 1)), mode="edge" if replicate else "constant")
+    a, b, c2 = xp[:, :-2, :-2], xp[:, :-2, 1:-1], xp[:, :-2, 2:]
+    d, e = xp[:, 1:-1, :-2], xp[:, 1:-1, 2:]
+    g, h, k = xp[:, 2:, :-2], xp[:, 2:, 1:-1], xp[:, 2:, 2:]
+    gx = ((-a + c2) + (-2.0 * d + 2.0 * e)) + (-g + k)
+    gy = ((-a - 2.0 * b) - c2) + ((g + 2.0 * h) + k)
+    s = 0.125 if normalized else 1.0
+    return gx * s, gy * s
+
+
+@pytest.mark.parametrize("shape,dtype,normalized,replicate", [
+    ((256, 240, 320), torch.float32, False, False),   # cfg2: 16-B vector loads, full tiles
+    ((130, 33, 100), torch.float32, True, True),      # partial channel block, W%32 != 0 (scalar edge tile)
+    ((9, 17, 131), torch.float32, False, True),       # W*4 not 16-B aligned: scalar loads throughout
+    ((70, 21, 66), torch.float64, True, False),       # fp64 input, 16-B (double2) vector loads
+    ((3, 5, 7), torch.float64, False, True),          # fewer rows than one tile
+])
+def test_pack_sobel_variants(shape, dtype, normalized, replicate):
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(shape, generator=g, dtype=dtype)
+    storage = torch.float64 if dtype == torch.float64 else torch.float32
+    feats = rf.pack_features(x, storage=storage, device=DEV, sobel_normalized=normalized,
+                             sobel_replicate_pad=replicate)
+    gx, gy = _sobel_np(x.double().numpy(), normalized, replicate)
+    buf = feats.buf.cpu().numpy()
+    C = shape[0]
+    np.testing.assert_array_equal(buf[:, :, 0, :C].transpose(2, 0, 1), x.numpy())
+    np.testing.assert_array_equal(buf[:, :, 1, :C].transpose(2, 0, 1), gx.astype(buf.dtype))
+    np.testing.assert_array_equal(buf[:, :, 2, :C].transpose(2, 0, 1), gy.astype(buf.dtype))
+    assert not buf[:, :, :, C:].any()
+    if not normalized and not replicate and dtype == torch.float32:
+        ogx, ogy = orc.sobel(x.double().numpy())
+        assert np.array_equal(ogx, gx) and np.array_equal(ogy, gy)
+
+
 def test_gather_reference_matches_oracle():
     z = load_npz("adapter_nonsquare")
     import json
