@@ -147,7 +147,7 @@ extern "C" {
 int fmpnp_abi_version(void) { return FMPNP_ABI_VERSION; }
 
 const char *fmpnp_build_info(void) {
-    return "fmpnp gfx950: lm_kernel(NT=512 wave-owned blocks, CH=16, NV=32, fp64 accumulation), pack_kernel(Sobel+HWC3), "
+    return "fmpnp gfx950: lm_kernel(NT=512 wave-owned blocks, CH=64, NV=32, fp64 accumulation), pack_kernel(Sobel+HWC3), "
            "gather_ref_kernel";
 }
 

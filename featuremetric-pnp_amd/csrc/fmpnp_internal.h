@@ -8,7 +8,7 @@
 namespace fmpnp {
 
 constexpr int NT = 512;         // threads per workgroup of the LM kernel (8 waves)
-constexpr int CH = 16;          // points per reduction chunk (fixed: results do not depend on G)
+constexpr int CH = 64;          // points per reduction chunk = one wave block (fixed: results do not depend on G)
 constexpr int NV = 32;          // reduced vector: 21 H + 6 g + rho + kept + supported + 2 pad
 constexpr int NSTAMP = 12;      // debug phase-stamp slots: 8 phases + eval-0 proj/gather/loss/contrib
 constexpr int RECW = 8;         // per-point record: 6 channel sums + rho + rho'
@@ -31,7 +31,7 @@ struct LaunchArgs {
     double *partials;             // [teams][2][nc_max][NV]
     double *maxslots;             // [teams][2][G]
     int mmax;                     // max points per workgroup (multiple of CH): dynamic LDS carve
-    unsigned long long *stamps;   // debug: [grid][NSTAMP] phase cycle totals, or null
+    unsigned long long *stamps;   // debug: [grid][8 waves][NSTAMP] phase cycle totals, or null
     int wps;                      // occupancy variant (WPS_LATENCY / WPS_THROUGHPUT)
 };
 

@@ -69,6 +69,35 @@ struct Ctx {
     int p0, M, c0, LC, NC;
 };
 
+// Per-problem constants of the point phases, held in registers (every value wave-uniform:
+// the compiler keeps them in SGPRs) instead of being re-read from the LDS Ctx at every use
+// -- each LDS read is a ~100-cycle round trip on the evaluation's critical path.
+struct PC {
+    const void *feat, *fref;
+    double K[9];
+    int Hf, Wf, cs, cb, ce, ld, im_w, im_h, p0, M, c0, LC, G;
+    UDiv dh, dw;
+    int loss, no_memo, use_ratio;
+    double alpha;
+    double *part_g;       // this team's partial slots [2][nc_max][NV] (G > 1)
+    int nc_max;
+    bool stamps;          // debug phase stamps on
+};
+
+__device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ unsigned ufirst(unsigned v) { return (unsigned)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ double ufirst(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <typename P>
+__device__ __forceinline__ P *ufirst(P *p) {
+    const uintptr_t b = (uintptr_t)p;
+    const unsigned lo = ufirst((unsigned)b), hi = ufirst((unsigned)(b >> 32));
+    return (P *)(((uintptr_t)hi << 32) | lo);
+}
+
 struct LMState {
     double R[9], t[3];      // current (last accepted) pose
     double Re[9], te[3];    // pose evaluated next
@@ -79,20 +108,44 @@ struct LMState {
     int best_inl, n_evals, n_steps, n_accepted, status, done, has_best, ret_current;
     int abort_flag, sync_ok;
     double wg_max[NT / 64];
-    unsigned long long stamp_t, stamp_ph[NSTAMP];  // debug phase stamps (lane 0)
+    unsigned long long stamp_t[NT / 64], stamp_ph[NT / 64][NSTAMP];  // debug phase stamps (lane 0 per wave)
     Ctx c;
 };
 static_assert(sizeof(LMState) <= lds_fixed_bytes(), "LDS head too small");
 
 __device__ __forceinline__ LMState &S() { return *reinterpret_cast<LMState *>(lm_lds); }
-// debug: add the cycles since the previous stamp to phase k (lane 0 of the workgroup only);
-// phases 0..3 of the first evaluation go to slots 8..11
-__device__ __forceinline__ void dbg_stamp(int k) {
+
+// Registers <- the LDS Ctx, once per problem (after problem_begin's barrier).
+__device__ __forceinline__ PC load_pc() {
+    const Ctx &c = S().c;
+    PC q;
+    q.feat = ufirst(c.feat);
+    q.fref = ufirst(c.fref);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) q.K[k] = ufirst(c.K[k]);
+    q.Hf = ufirst(c.Hf); q.Wf = ufirst(c.Wf); q.cs = ufirst(c.cs); q.cb = ufirst(c.cb); q.ce = ufirst(c.ce);
+    q.ld = ufirst(c.ld_ref); q.im_w = ufirst(c.im_w); q.im_h = ufirst(c.im_h); q.p0 = ufirst(c.p0);
+    q.M = ufirst(c.M); q.c0 = ufirst(c.c0); q.LC = ufirst(c.LC); q.G = ufirst(c.G);
+    q.dh = UDiv{ufirst(c.div_h.m), ufirst(c.div_h.s1), ufirst(c.div_h.s2)};
+    q.dw = UDiv{ufirst(c.div_w.m), ufirst(c.div_w.s1), ufirst(c.div_w.s2)};
+    q.loss = ufirst(c.mode == FMPNP_MODE_COMPUTE_COST ? (int)FMPNP_SQUARED : c.loss);
+    q.no_memo = ufirst(c.no_memo);
+    q.use_ratio = ufirst(c.use_ratio);
+    q.alpha = ufirst(c.alpha);
+    q.part_g = ufirst(c.part_g);
+    q.nc_max = ufirst(c.nc_max);
+    q.stamps = ufirst(c.stamps_on) != 0;
+    return q;
+}
+// debug: add the cycles since the wave's previous stamp to its phase k (lane 0 of each
+// wave); phases 0..3 of the first evaluation go to slots 8..11
+__device__ __forceinline__ void dbg_stamp(bool on, int k) {
     LMState &st = *reinterpret_cast<LMState *>(lm_lds);
-    if (st.c.stamps_on && threadIdx.x == 0) {
+    if (on && (threadIdx.x & 63) == 0) {
+        const int w = threadIdx.x >> 6;
         const unsigned long long now = __builtin_amdgcn_s_memtime();
-        st.stamp_ph[k < 4 && st.n_evals == 0 ? 8 + k : k] += now - st.stamp_t;
-        st.stamp_t = now;
+        st.stamp_ph[w][k < 4 && st.n_evals == 0 ? 8 + k : k] += now - st.stamp_t[w];
+        st.stamp_t[w] = now;
     }
 }
 __device__ __forceinline__ unsigned char *dyn() { return lm_lds + lds_fixed_bytes(); }
@@ -375,6 +428,33 @@ __device__ __forceinline__ double reduce8_in16(double v[8], int l16) {
     return v[0] + dpp64<DPP_XOR1>(v[0]);
 }
 
+// Transposed reduction of the 32-value vector over all 64 lanes of a wave.  `val(k)`
+// yields value k of the lane; values are produced in pairs (i, i+16) and folded at once by
+// the permlane32 swap (bit 5), so at most 16 doubles are live; then bit 4 (permlane16 swap)
+// and the in-row DPP steps.  Lane l returns the wave total of value index
+// 16*b5 + 8*b4 + 4*b3 + 2*b2 + b1 (b0 duplicates).  Only equal indices are ever added.
+template <typename F>
+__device__ __forceinline__ double reduce32_in64(F &&val, int lane) {
+    double v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        double a = val(i), b = val(i + 16);
+        swap32(a, b);  // low half keeps index i, high half i + 16
+        v[i] = a + b;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        double a = v[i], b = v[i + 8];
+        swap16(a, b);  // even rows keep index i, odd rows i + 8
+        v[i] = a + b;
+    }
+    return reduce8_in16(v, lane & 15);
+}
+__device__ __forceinline__ int reduce32_index(int lane) {
+    return 16 * ((lane >> 5) & 1) + 8 * ((lane >> 4) & 1) + 4 * ((lane >> 3) & 1) + 2 * ((lane >> 2) & 1) +
+           ((lane >> 1) & 1);
+}
+
 // ---------------------------------------------------------------------------
 // Ratio test (model.py:120-129): the team's max |rho| (order-free: exact) from every
 // wave's maximum.  Returns false on abort.
@@ -417,14 +497,13 @@ __device__ __forceinline__ constexpr int h_col(int k) {
 }
 
 // One 64-point block of a wave: lane = point.  Points that do not contribute get w = 0
-// and a harmless geometry (z = 1).  Writes the block's four chunk partials.
-__device__ __forceinline__ void contrib_block(int mmax, int blk, bool sup, bool kept, double rho, double d1,
-                                              const double *r, const double Pc[3]) {
-    LMState &st = S();
-    const Ctx &c = st.c;
-    const int lane = threadIdx.x & 63, l16 = lane & 15;
-    const double fx = c.K[0], fy = c.K[4];
-    const int lc = blk * 4 + (lane >> 4);
+// and a harmless geometry (z = 1).  Writes the block's partial (one chunk: LDS when
+// G == 1, the team's global slot `dst_g` with sc1 stores when G > 1).
+__device__ __forceinline__ void contrib_block(const PC &q, int mmax, int blk, bool sup, bool kept, double rho,
+                                              double d1, const double *r, const double Pc[3], double *dst_g) {
+    const int lane = threadIdx.x & 63;
+    const double fx = q.K[0], fy = q.K[4];
+    const int lc = blk;  // one chunk per 64-point block
     const double w = kept ? d1 : 0.0, rh = kept ? rho : 0.0;
     const double P0 = kept ? Pc[0] : 0.0, P1 = kept ? Pc[1] : 0.0, z = kept ? Pc[2] : 1.0;
     const double sex = kept ? r[1] : 0.0, sey = kept ? r[2] : 0.0;
@@ -449,67 +528,121 @@ __device__ __forceinline__ void contrib_block(int mmax, int blk, bool sup, bool 
         M0[l] = wxx * A0[l] + wxy * A1[l];
         M1[l] = wxy * A0[l] + wyy * A1[l];
     }
-    double *dst_l = lds_part(mmax) + (size_t)(c.c0 + lc) * NV;  // G == 1 (the LDS address space)
-    double *dst_g = c.part_g + (size_t)((c.epoch + 1) & 1) * c.nc_max * NV + (size_t)(c.c0 + lc) * NV;
-    // the 32-value vector in four quarters of 8: only 8 doubles live per reduction
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        double v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int k = 8 * q + e;
-            if (k < 21) {  // H[a][b] = A_a^T (w S) A_b
-                const int a = h_row(k), b = h_col(k);
-                v[e] = a == 0 ? A0[0] * M0[b] : a == 1 ? A1[1] * M1[b] : A0[a] * M0[b] + A1[a] * M1[b];
-            } else if (k < 27) {  // g = A^T (w G^T e)
-                const int l = k - 21;
-                v[e] = l == 0 ? A0[0] * wex : l == 1 ? A1[1] * wey : A0[l] * wex + A1[l] * wey;
-            } else if (k == 27) {
-                v[e] = rh;
-            } else if (k == 28) {
-                v[e] = kept ? 1.0 : 0.0;
-            } else if (k == 29) {
-                v[e] = sup ? 1.0 : 0.0;
-            } else {
-                v[e] = 0.0;
-            }
+    auto val = [&](int k) -> double {
+        if (k < 21) {  // H[a][b] = A_a^T (w S) A_b
+            const int a = h_row(k), b = h_col(k);
+            return a == 0 ? A0[0] * M0[b] : a == 1 ? A1[1] * M1[b] : A0[a] * M0[b] + A1[a] * M1[b];
+        } else if (k < 27) {  // g = A^T (w G^T e)
+            const int l = k - 21;
+            return l == 0 ? A0[0] * wex : l == 1 ? A1[1] * wey : A0[l] * wex + A1[l] * wey;
+        } else if (k == 27) {
+            return rh;
+        } else if (k == 28) {
+            return kept ? 1.0 : 0.0;
+        } else if (k == 29) {
+            return sup ? 1.0 : 0.0;
         }
-        const double tot = reduce8_in16(v, l16);
-        const int idx = 8 * q + 4 * ((l16 >> 3) & 1) + 2 * ((l16 >> 2) & 1) + ((l16 >> 1) & 1);
-        if (lc < c.LC && (l16 & 1) == 0) {
-            if (c.G == 1) dst_l[idx] = tot;
-            else st_sc1(dst_g + idx, tot);
-        }
+        return 0.0;
+    };
+    const double tot = reduce32_in64(val, lane);
+    if (lc < q.LC && (lane & 1) == 0) {
+        const int idx = reduce32_index(lane);
+        if (q.G == 1) lds_part(mmax)[(size_t)(q.c0 + lc) * NV + idx] = tot;  // G == 1 (LDS)
+        else st_sc1(dst_g + (size_t)(q.c0 + lc) * NV + idx, tot);
     }
+}
+
+// The eight 16-byte loads of one point's texel for one half-wave lane (C <= 64 V channels:
+// a point is one memory round trip), issued ahead of their use so that the next pair's
+// loads are in flight while the current pair is reduced.
+template <typename T>
+struct GLoad {
+    typename V16<T>::type f0, x0, y0, q0, f1, x1, y1, q1;
+};
+template <typename T>
+__device__ __forceinline__ void g_issue(GLoad<T> &g, const T *t, const T *rf, int cs, int c, int c2) {
+    using VT = typename V16<T>::type;
+    g.f0 = gload<VT>(t + c);
+    g.x0 = gload<VT>(t + cs + c);
+    g.y0 = gload<VT>(t + 2 * cs + c);
+    g.q0 = gload<VT>(rf + c);
+    g.f1 = gload<VT>(t + c2);
+    g.x1 = gload<VT>(t + cs + c2);
+    g.y1 = gload<VT>(t + 2 * cs + c2);
+    g.q1 = gload<VT>(rf + c2);
+}
+// Same accumulation order as gather_half<T, true> (round one, then round two or exact
+// zeros), so both paths give bit-identical sums; has1 = false lanes add nothing.
+template <typename T>
+__device__ __forceinline__ void g_consume(const GLoad<T> &g, bool has1, bool has2, double a[8]) {
+    constexpr int V = V16<T>::n;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = 0.0;
+    if (!has1) return;
+    const T *pf = reinterpret_cast<const T *>(&g.f0), *px = reinterpret_cast<const T *>(&g.x0);
+    const T *py = reinterpret_cast<const T *>(&g.y0), *pr = reinterpret_cast<const T *>(&g.q0);
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc6(a, (double)pf[k], (double)pr[k], (double)px[k], (double)py[k]);
+    const T *sf = reinterpret_cast<const T *>(&g.f1), *sx = reinterpret_cast<const T *>(&g.x1);
+    const T *sy = reinterpret_cast<const T *>(&g.y1), *sr = reinterpret_cast<const T *>(&g.q1);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        const double z = 0.0;
+        acc6(a, has2 ? (double)sf[k] : z, has2 ? (double)sr[k] : z, has2 ? (double)sx[k] : z,
+             has2 ? (double)sy[k] : z);
+    }
+}
+
+// Pair selection from a dirty mask: the half-waves take the two lowest set lanes.
+struct GPair {
+    int j;      // this half-wave's point (lane index in the block)
+    int to;     // its texel offset
+    bool two;   // a second point exists (the high half's point is real)
+};
+__device__ __forceinline__ GPair pick_pair(unsigned long long &m, int off, bool hi) {
+    const int a = __builtin_ctzll(m);
+    m &= m - 1;
+    const bool two = m != 0;
+    const int b = two ? __builtin_ctzll(m) : a;
+    if (two) m &= m - 1;
+    const int oa = __builtin_amdgcn_readlane(off, a), ob = __builtin_amdgcn_readlane(off, b);
+    return GPair{hi ? b : a, hi ? ob : oa, two};
 }
 
 // ---------------------------------------------------------------------------
 // One evaluation at (Re, te) over the wave's blocks (no workgroup barrier inside).
 // Without the ratio test each block goes straight on to its chunk partials; with it the
 // loss values are parked in the records and the wave's max |rho| is returned.
+// PIPE: double-buffered gathers (latency variant: the VGPRs for two pairs in flight).
 // ---------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ double eval_pass(int mmax, long long &ngath) {
+template <typename T, bool PIPE>
+__device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ngath) {
     LMState &st = S();
-    const Ctx &c = st.c;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l32 = lane & 31;
     const bool hi = lane >= 32;
     const double *X = lds_X(mmax);
     double *rec = lds_rec(mmax);
     int *tex = lds_tex(mmax);
-    const T *feat = reinterpret_cast<const T *>(c.feat);
-    const T *fref = reinterpret_cast<const T *>(c.fref);
-    const int cs = c.cs, cb = c.cb, ce = c.ce, p0 = c.p0, ld = c.ld_ref, M = c.M;
+    const T *feat = reinterpret_cast<const T *>(q.feat);
+    const T *fref = reinterpret_cast<const T *>(q.fref);
+    const int cs = q.cs, cb = q.cb, ce = q.ce, p0 = q.p0, ld = q.ld, M = q.M;
     constexpr int V = V16<T>::n;
     const bool vec = ((((uintptr_t)feat) | ((uintptr_t)fref)) & 15) == 0 && cs % V == 0 && ld % V == 0 &&
                      cb % V == 0 && (ce - cb) % V == 0;
-    const int loss = c.mode == FMPNP_MODE_COMPUTE_COST ? (int)FMPNP_SQUARED : c.loss;
-    const bool defer = c.use_ratio != 0;
+    // one round trip per point: every channel of the slice within the two rounds of a lane
+    const bool onetrip = vec && ce - cb <= 64 * V;
+    const int gc = cb + l32 * V;                    // this lane's first channel (one-trip path)
+    const bool has1 = gc < ce, has2 = gc + 32 * V < ce;
+    const int gc1 = has1 ? gc : cb, gc2 = has2 ? gc + 32 * V : gc1;
+    const bool defer = q.use_ratio != 0;
+    double *dst_g = q.part_g;
+    if (q.G > 1) dst_g += (size_t)((ufirst((int)st.c.epoch) + 1) & 1) * q.nc_max * NV;
+    // the pose evaluated: uniform, one LDS read per evaluation
     double Re[9], te[3];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Re[k] = st.Re[k];
+    for (int k = 0; k < 9; ++k) Re[k] = ufirst(st.Re[k]);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) te[k] = st.te[k];
+    for (int k = 0; k < 3; ++k) te[k] = ufirst(st.te[k]);
     double lmax = -1.0;  // -1: nothing supported seen yet
     for (int blk = wave; blk * 64 < M; blk += NT / 64) {
         const int i = blk * 64 + lane;
@@ -523,48 +656,82 @@ __device__ __forceinline__ double eval_pass(int mmax, long long &ngath) {
         if (valid) {
             transform_pt(Re, te, X[3 * i], X[3 * i + 1], X[3 * i + 2], Pc);
             int x, y;
-            if (project_px(c.K, Pc, c.im_w, c.im_h, x, y)) {
-                const int row = (int)udiv((unsigned)y * (unsigned)c.Hf, c.div_h);
-                const int col = (int)udiv((unsigned)x * (unsigned)c.Wf, c.div_w);
-                off = row * c.Wf + col;
+            if (project_px(q.K, Pc, q.im_w, q.im_h, x, y)) {
+                const int row = (int)udiv((unsigned)y * (unsigned)q.Hf, q.dh);
+                const int col = (int)udiv((unsigned)x * (unsigned)q.Wf, q.dw);
+                off = row * q.Wf + col;
             }
         }
         // memoised gather: a point whose texel did not change keeps its record (the six
         // channel sums depend only on the texel and the point's fixed descriptor)
         const int old = valid ? tex[i] : -1;
-        const bool dirty = off >= 0 && (off != old || c.no_memo);
+        const bool dirty = off >= 0 && (off != old || q.no_memo);
         if (valid) tex[i] = off;
         unsigned long long m = __ballot(dirty);
         ngath += __popcll(m);
-        dbg_stamp(0);
-        while (m) {  // wave-uniform: two dirty points per trip, one per half-wave
-            const int a = __builtin_ctzll(m);
-            m &= m - 1;
-            const bool two = m != 0;
-            const int b = two ? __builtin_ctzll(m) : a;
-            if (two) m &= m - 1;
-            const int oa = __builtin_amdgcn_readlane(off, a), ob = __builtin_amdgcn_readlane(off, b);
-            const int j = hi ? b : a, to = hi ? ob : oa;
-            const int ii = blk * 64 + j;
-            const T *t = feat + (size_t)to * 3 * cs;
-            const T *rf = fref + (size_t)(p0 + ii) * ld;
-            double v[8];
+        dbg_stamp(q.stamps, 0);
+        const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
+        const bool wlane = (lane & 3) == 0 && e6 < 6;
+        if (PIPE && onetrip) {
+            // double-buffered pairs: the next pair's loads are issued before this pair's
+            // channel sums are reduced (one exposed round trip per block, not one per pair)
+            if (m) {
+                GLoad<T> A, B;
+                GPair pa = pick_pair(m, off, hi), pb;
+                g_issue<T>(A, feat + (size_t)pa.to * 3 * cs, fref + (size_t)(p0 + blk * 64 + pa.j) * ld, cs, gc1,
+                           gc2);
+                while (true) {
+                    const bool moreB = m != 0;
+                    if (moreB) {
+                        pb = pick_pair(m, off, hi);
+                        g_issue<T>(B, feat + (size_t)pb.to * 3 * cs, fref + (size_t)(p0 + blk * 64 + pb.j) * ld,
+                                   cs, gc1, gc2);
+                    }
+                    {
+                        double v[8];
+                        g_consume<T>(A, has1, has2, v);
+                        const double r = reduce8_in32(v, lane);
+                        if (wlane && (!hi || pa.two)) rec[(size_t)(blk * 64 + pa.j) * RECW + e6] = r;
+                    }
+                    if (!moreB) break;
+                    const bool moreA = m != 0;
+                    if (moreA) {
+                        pa = pick_pair(m, off, hi);
+                        g_issue<T>(A, feat + (size_t)pa.to * 3 * cs, fref + (size_t)(p0 + blk * 64 + pa.j) * ld,
+                                   cs, gc1, gc2);
+                    }
+                    {
+                        double v[8];
+                        g_consume<T>(B, has1, has2, v);
+                        const double r = reduce8_in32(v, lane);
+                        if (wlane && (!hi || pb.two)) rec[(size_t)(blk * 64 + pb.j) * RECW + e6] = r;
+                    }
+                    if (!moreA) break;
+                }
+            }
+        } else {
+            while (m) {  // wave-uniform: two dirty points per trip, one per half-wave
+                const GPair pp = pick_pair(m, off, hi);
+                const int ii = blk * 64 + pp.j;
+                const T *t = feat + (size_t)pp.to * 3 * cs;
+                const T *rf = fref + (size_t)(p0 + ii) * ld;
+                double v[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = 0.0;
-            if (vec) gather_half<T, true>(t, rf, cs, cb, ce, l32, v);
-            else gather_half<T, false>(t, rf, cs, cb, ce, l32, v);
-            const double r = reduce8_in32(v, lane);
-            const int e = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
-            if ((lane & 3) == 0 && e < 6 && (!hi || two)) rec[(size_t)ii * RECW + e] = r;
+                for (int e = 0; e < 8; ++e) v[e] = 0.0;
+                if (vec) gather_half<T, true>(t, rf, cs, cb, ce, l32, v);
+                else gather_half<T, false>(t, rf, cs, cb, ce, l32, v);
+                const double r = reduce8_in32(v, lane);
+                if (wlane && (!hi || pp.two)) rec[(size_t)ii * RECW + e6] = r;
+            }
         }
         // the records just written are read by other lanes of this wave: LDS operations of
         // a wave complete in order; the clobber keeps the compiler from reordering them
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        dbg_stamp(1);
+        dbg_stamp(q.stamps, 1);
         const bool sup = off >= 0;
         const double *r = rec + (size_t)(valid ? i : 0) * RECW;
         double rho = 0.0, d1 = 0.0;
-        if (sup) loss_eval(loss, c.alpha, 0.5 * r[0], rho, d1);
+        if (sup) loss_eval(q.loss, q.alpha, 0.5 * r[0], rho, d1);
         if (defer) {
             if (valid) {
                 rec[(size_t)i * RECW + 6] = rho;
@@ -572,95 +739,80 @@ __device__ __forceinline__ double eval_pass(int mmax, long long &ngath) {
             }
             if (sup) lmax = nanmax(lmax, fabs(rho));
         } else {
-            contrib_block(mmax, blk, sup, sup, rho, d1, r, Pc);
+            contrib_block(q, mmax, blk, sup, sup, rho, d1, r, Pc, dst_g);
         }
-        dbg_stamp(2);
+        dbg_stamp(q.stamps, 2);
     }
     return lmax;
 }
 
 // Second pass of the ratio test: the weights of points with |rho| >= max|rho| * thr
 // are zero (model.py:324-336); P is recomputed bit-identically from X.
-__device__ __forceinline__ void contrib_pass(int mmax) {
+__device__ __forceinline__ void contrib_pass(const PC &q, int mmax) {
     LMState &st = S();
-    const Ctx &c = st.c;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const double *X = lds_X(mmax);
     const double *rec = lds_rec(mmax);
     const int *tex = lds_tex(mmax);
-    const double limit = st.rho_max * c.ratio_thr;
+    const double limit = ufirst(st.rho_max) * st.c.ratio_thr;
+    double *dst_g = q.part_g;
+    if (q.G > 1) dst_g += (size_t)((ufirst((int)st.c.epoch) + 1) & 1) * q.nc_max * NV;
     double Re[9], te[3];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Re[k] = st.Re[k];
+    for (int k = 0; k < 9; ++k) Re[k] = ufirst(st.Re[k]);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) te[k] = st.te[k];
-    for (int blk = wave; blk * 64 < c.M; blk += NT / 64) {
+    for (int k = 0; k < 3; ++k) te[k] = ufirst(st.te[k]);
+    for (int blk = wave; blk * 64 < q.M; blk += NT / 64) {
         const int i = blk * 64 + lane;
-        const bool valid = i < c.M;
+        const bool valid = i < q.M;
         const bool sup = valid && tex[i] >= 0;
         double Pc[3] = {0.0, 0.0, 1.0};
         if (sup) transform_pt(Re, te, X[3 * i], X[3 * i + 1], X[3 * i + 2], Pc);
         const double *r = rec + (size_t)(valid ? i : 0) * RECW;
         const bool kept = sup && fabs(r[6]) < limit;
-        contrib_block(mmax, blk, sup, kept, r[6], r[7], r, Pc);
+        contrib_block(q, mmax, blk, sup, kept, r[6], r[7], r, Pc, dst_g);
     }
 }
 
 // ---------------------------------------------------------------------------
 // Combine on wave 0 (after the barrier / team exchange): the ordered sum over chunk
-// indices.  Row q of NQ = 32 rows sums chunks q, q+32, ... in chunk order; a fixed
-// pairwise tree over the rows follows (lane l: value l&31, rows 16*(l>>5) .. +15; the
-// halves are added across the wave).  Depends only on the chunk partials and NC -- not
-// on G, placement or timing.
+// (= block) indices.  Lane (j, h) (value j = lane & 31, half h = lane >> 5) sums chunks
+// h, h+2, h+4, ... in order; the halves are then added.  Depends only on the chunk
+// partials and NC -- not on G, placement or timing.
 // ---------------------------------------------------------------------------
-constexpr int NQ = 32;
-
-__device__ __forceinline__ void combine_final_wave(int mmax) {
+__device__ __forceinline__ double combine_final_wave(int mmax) {
     LMState &st = S();
     const Ctx &c = st.c;
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
     const int NC = c.NC;
-    double t[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) t[q] = 0.0;
-    // rounds of 32 chunks: the 16 loads of a round are issued before their adds; per row
-    // the adds stay in chunk order
+    double t = 0.0;
     if (c.G == 1) {
         const double *src = lds_part(mmax);
-        for (int r0 = 0; r0 < NC; r0 += NQ) {
-            double v[16];
+        double v[4];
+        for (int r0 = h; r0 < NC; r0 += 8) {  // four loads in flight, adds in chunk order
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int ch = r0 + 16 * h + q;
-                v[q] = ch < NC ? src[ch * NV + j] : 0.0;
-            }
+            for (int u = 0; u < 4; ++u) v[u] = r0 + 2 * u < NC ? src[(r0 + 2 * u) * NV + j] : 0.0;
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
-                if (r0 + 16 * h + q < NC) t[q] += v[q];
+            for (int u = 0; u < 4; ++u)
+                if (r0 + 2 * u < NC) t += v[u];
         }
     } else {
         const double *src = c.part_g + (size_t)(c.epoch & 1) * c.nc_max * NV;
-        for (int r0 = 0; r0 < NC; r0 += NQ) {
-            double v[16];
+        double v[4];
+        for (int r0 = h; r0 < NC; r0 += 8) {
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int ch = r0 + 16 * h + q;
-                v[q] = ch < NC ? ld_sc1(src + ch * NV + j) : 0.0;
-            }
+            for (int u = 0; u < 4; ++u) v[u] = r0 + 2 * u < NC ? ld_sc1(src + (r0 + 2 * u) * NV + j) : 0.0;
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
-                if (r0 + 16 * h + q < NC) t[q] += v[q];
+            for (int u = 0; u < 4; ++u)
+                if (r0 + 2 * u < NC) t += v[u];
         }
     }
-#pragma unroll
-    for (int w = 1; w < 16; w *= 2)
-#pragma unroll
-        for (int q = 0; q < 16; q += 2 * w) t[q] = t[q] + t[q + w];
-    double a = t[0], b = t[0];
+    double a = t, b = t;
     swap32(a, b);  // low half: (own, partner); high half: (partner, own)
-    const double tot = a + b;  // rows 0..15 + rows 16..31 in both halves
+    const double tot = a + b;  // even chunks + odd chunks, in both halves
     if (lane < NV) st.tot[lane] = tot;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back by this wave only
+    return tot;
 }
 
 // ---------------------------------------------------------------------------
@@ -891,12 +1043,12 @@ __device__ __forceinline__ void lm_update_wave() {
     }
     // next step from the linearisation at the current pose (model.py:408-426)
     double delta[6];
-    dbg_stamp(5);  // LM bookkeeping
+    dbg_stamp(c.stamps_on != 0, 5);  // LM bookkeeping
     {
         const double *Hu = take ? st.tot : st.Hc, *gv = take ? st.tot + 21 : st.gc;
         if (!ldlt_step(Hu, gv, lambda, lr, delta)) lm_step_rows(Hu, gv, lambda, lr, delta);
     }
-    dbg_stamp(6);  // 6x6 solve
+    dbg_stamp(c.stamps_on != 0, 6);  // 6x6 solve
     bool bad = false;
 #pragma unroll
     for (int k = 0; k < 6; ++k) bad |= isnan(delta[k]);
@@ -965,29 +1117,31 @@ __global__ __launch_bounds__(NT, WPS) void lm_kernel(LaunchArgs a) {
     __syncthreads();
     // optional phase stamps (debug: a.stamps != null): s_memtime deltas on thread 0
     const bool stamps_on = a.stamps != nullptr;
-    if (stamps_on && tid == 0) {
-        for (int k = 0; k < NSTAMP; ++k) st.stamp_ph[k] = 0;
-        st.stamp_t = __builtin_amdgcn_s_memtime();
+    if (stamps_on && (tid & 63) == 0) {
+        for (int k = 0; k < NSTAMP; ++k) st.stamp_ph[tid >> 6][k] = 0;
+        st.stamp_t[tid >> 6] = __builtin_amdgcn_s_memtime();
     }
     for (int p = team; p < a.n; p += a.teams) {
         problem_begin(a.probs + p, p, mmax);
+        const PC q = load_pc();
         long long ngath = 0;  // texel gathers of this wave for this problem
         while (!st.done) {
-            const double lmax = eval_pass<T>(mmax, ngath);  // project, gather, loss (+ partials)
-            if (st.c.use_ratio) {
+            // project, gather, loss (+ partials)
+            const double lmax = eval_pass<T, WPS == WPS_LATENCY>(q, mmax, ngath);
+            if (q.use_ratio) {
                 if (!ratio_exchange(lmax)) break;
-                contrib_pass(mmax);
+                contrib_pass(q, mmax);
             }
             if (st.c.G > 1) team_arrive();
             else __syncthreads();
             if (tid < 64 && (st.c.G == 1 || team_wait())) {
-                dbg_stamp(3);  // slowest wave + exchange
+                dbg_stamp(q.stamps, 3);  // slowest wave + exchange
                 combine_final_wave(mmax);
-                dbg_stamp(4);
+                dbg_stamp(q.stamps, 4);
                 lm_update_wave();
             }
             __syncthreads();
-            dbg_stamp(7);  // pose update + barrier
+            dbg_stamp(q.stamps, 7);  // pose update + barrier
             if (st.abort_flag) break;
         }
         // every wave of every team member adds its share (results are zeroed by the launcher)
@@ -996,8 +1150,9 @@ __global__ __launch_bounds__(NT, WPS) void lm_kernel(LaunchArgs a) {
                       (unsigned long long)ngath);
         problem_end();
     }
-    if (stamps_on && tid == 0)
-        for (int k = 0; k < NSTAMP; ++k) a.stamps[(size_t)blockIdx.x * NSTAMP + k] = st.stamp_ph[k];
+    if (stamps_on && (tid & 63) == 0)
+        for (int k = 0; k < NSTAMP; ++k)
+            a.stamps[((size_t)blockIdx.x * (NT / 64) + (tid >> 6)) * NSTAMP + k] = st.stamp_ph[tid >> 6][k];
 }
 
 template __global__ void lm_kernel<float, WPS_LATENCY>(LaunchArgs);

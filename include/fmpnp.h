@@ -159,8 +159,9 @@ int fmpnp_refine_batch(const fmpnp_problem *probs_host, int n, const fmpnp_optio
                        fmpnp_trace_entry *trace, int trace_stride, void *hip_stream);
 
 /* Debug: when device_buf != NULL, later LM launches write per-workgroup phase cycle
- * totals (s_memtime) to device_buf[grid][12] (8 phases, then the first evaluation's projection,
- * gather, loss and contribution phases separately); NULL switches it off. */
+ * totals (s_memtime) to device_buf[grid][8 waves][12] (8 phases, then the first evaluation's
+ * projection, gather, loss and contribution phases separately; phases 3-7 are wave 0's LM tail);
+ * NULL switches it off. */
 int fmpnp_debug_stamps(unsigned long long *device_buf);
 
 /* Last launch geometry of this thread (for benches / tests). */

@@ -19,7 +19,7 @@ ab.launch(); torch.cuda.synchronize()
 L = _lib.load()
 L.fmpnp_debug_stamps.argtypes = [ctypes.c_void_p]
 info = _lib.last_launch()
-st = torch.zeros(info["grid"] * 12, dtype=torch.int64, device=dev)
+st = torch.zeros(info["grid"] * 8 * 12, dtype=torch.int64, device=dev)
 L.fmpnp_debug_stamps(ctypes.c_void_p(st.data_ptr()))
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record(); ab.launch(); e1.record(); torch.cuda.synchronize()
@@ -29,7 +29,8 @@ for _ in range(10):
     e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e2.record(); ab.launch(); e3.record(); torch.cuda.synchronize()
     plain.append(e2.elapsed_time(e3))
-ph = st.view(-1, 12).cpu().numpy().astype(np.float64)
+phw = st.view(-1, 8, 12).cpu().numpy().astype(np.float64)
+ph = phw[:, 0, :]
 res = ab.results()
 g = sum(r["texel_gathers"] for r in res)
 full = sum(r["n_evals"] for r in res) * 512
@@ -40,3 +41,8 @@ tot = ph.sum(0)
 print(f"B={B} launch={info} stamped launch {e0.elapsed_time(e1):.3f} ms, plain launch median {np.median(plain):.3f} ms (min {min(plain):.3f}) -> {B / np.median(plain) * 1e3:.0f} /s")
 for k in range(12):
     print(f"  {names[k]:12s} {100 * tot[k] / tot.sum():6.2f} %   mean per WG {ph[:, k].mean() / 1e3:10.1f} kcyc")
+evals = sum(r["n_evals"] for r in res) / max(len(res), 1)
+print(f"per-wave phases 0-2 (steady state, cycles per evaluation, mean over WGs; {evals:.0f} evals/problem):")
+for w in range(8):
+    v = phw[:, w, :3].mean(0) / max(evals - 1, 1)
+    print(f"  wave {w}: proj {v[0]:7.0f}  gather {v[1]:7.0f}  loss+contrib {v[2]:7.0f}  sum {v.sum():7.0f}")
