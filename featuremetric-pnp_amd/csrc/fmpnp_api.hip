@@ -81,7 +81,9 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     // (MI355X_MICROARCH.md, Residency) -> min(api, 6).
     auto occupancy = [&](int lds) {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lm_kernel_ptr(opt->dtype, P.wps), NT, lds) !=
+        const bool gm = opt->loss == FMPNP_GEMAN_MCCLURE && opt->mode == FMPNP_MODE_FORWARD;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lm_kernel_ptr(opt->dtype, P.wps, P.G > 1, opt->use_ratio != 0, gm),
+                                                         NT, lds) !=
             hipSuccess)
             return 1;
         return std::max(1, std::min(nb, 6));

@@ -40,7 +40,7 @@ __host__ __device__ constexpr int lds_fixed_bytes() { return 4096; }
 size_t lm_dyn_lds_bytes(int mmax, int nc_max);
 
 hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream);
-const void *lm_kernel_ptr(int dtype, int wps);
+const void *lm_kernel_ptr(int dtype, int wps, bool team, bool ratio, bool gm);
 
 hipError_t launch_pack(const void *chw, const void *gx, const void *gy, int dtype_in, int C, int H, int W, void *out,
                        int dtype_out, int cstride, int normalized, int replicate, hipStream_t stream);

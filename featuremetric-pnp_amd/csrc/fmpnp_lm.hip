@@ -160,6 +160,32 @@ __device__ __forceinline__ double *lds_part(int mmax) {
     return reinterpret_cast<double *>(dyn()) + (3 + RECW) * mmax + ((mmax + 3) / 4) * 2;
 }
 
+// sin, cos of 0 <= x <= pi/4 by Horner-form Taylor series to x^17 / x^18 (truncation
+// below 1e-19 relative; a few ulp of rounding): ~20 register-resident fp64 operations
+// instead of the library's range-reduced sincos on the LM tail's critical path.
+__device__ __forceinline__ void sincos_small(double x, double &s, double &c) {
+    const double z = x * x;
+    double ps = 1.0 / 355687428096000.0;
+    ps = fma(ps, z, -1.0 / 1307674368000.0);
+    ps = fma(ps, z, 1.0 / 6227020800.0);
+    ps = fma(ps, z, -1.0 / 39916800.0);
+    ps = fma(ps, z, 1.0 / 362880.0);
+    ps = fma(ps, z, -1.0 / 5040.0);
+    ps = fma(ps, z, 1.0 / 120.0);
+    ps = fma(ps, z, -1.0 / 6.0);
+    s = fma(x * z, ps, x);
+    double pc = -1.0 / 6402373705728000.0;
+    pc = fma(pc, z, 1.0 / 20922789888000.0);
+    pc = fma(pc, z, -1.0 / 87178291200.0);
+    pc = fma(pc, z, 1.0 / 479001600.0);
+    pc = fma(pc, z, -1.0 / 3628800.0);
+    pc = fma(pc, z, 1.0 / 40320.0);
+    pc = fma(pc, z, -1.0 / 720.0);
+    pc = fma(pc, z, 1.0 / 24.0);
+    pc = fma(pc, z, -0.5);
+    c = fma(z, pc, 1.0);
+}
+
 // so3exp_map (helpers/utils.py:209-221) and the update R' = dR R, t' = dR t + dt
 // (model.py:416-426).
 __device__ __forceinline__ void pose_update(const double *R, const double *t, const double delta[6], double *Rn,
@@ -175,7 +201,8 @@ __device__ __forceinline__ void pose_update(const double *R, const double *t, co
         const double k0 = w0 * it, k1 = w1 * it, k2 = w2 * it;
         const double W[9] = {0, -k2, k1, k2, 0, -k0, -k1, k0, 0};
         double s, c;
-        sincos(theta, &s, &c);
+        if (theta <= 0.78539816339744828) sincos_small(theta, s, c);
+        else sincos(theta, &s, &c);
         const double c1 = 1.0 - c;
 #pragma unroll
         for (int i = 0; i < 3; ++i)
@@ -780,13 +807,13 @@ __device__ __forceinline__ void contrib_pass(const PC &q, int mmax) {
 // h, h+2, h+4, ... in order; the halves are then added.  Depends only on the chunk
 // partials and NC -- not on G, placement or timing.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double combine_final_wave(int mmax) {
+__device__ __forceinline__ double combine_final_wave(int mmax, bool team) {
     LMState &st = S();
     const Ctx &c = st.c;
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
     const int NC = c.NC;
     double t = 0.0;
-    if (c.G == 1) {
+    if (!team) {
         const double *src = lds_part(mmax);
         double v[4];
         for (int r0 = h; r0 < NC; r0 += 8) {  // four loads in flight, adds in chunk order
@@ -1078,7 +1105,10 @@ __device__ __forceinline__ void lm_update_wave() {
 // ---------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------
-template <typename T, int WPS>
+// Specialised per launch (the launcher picks the variant): TEAM = G > 1, RATIO = the ratio
+// test is on, GM = Geman-McClure forward (the common case) -- constant-folding the other
+// paths out shortens the per-point code and frees registers.
+template <typename T, int WPS, bool TEAM, bool RATIO, bool GM>
 __global__ __launch_bounds__(NT, WPS) void lm_kernel(LaunchArgs a) {
     LMState &st = S();
     const int G = a.G;
@@ -1123,7 +1153,10 @@ __global__ __launch_bounds__(NT, WPS) void lm_kernel(LaunchArgs a) {
     }
     for (int p = team; p < a.n; p += a.teams) {
         problem_begin(a.probs + p, p, mmax);
-        const PC q = load_pc();
+        PC q = load_pc();
+        if constexpr (!TEAM) q.G = 1;
+        q.use_ratio = RATIO ? 1 : 0;
+        if constexpr (GM) q.loss = FMPNP_GEMAN_MCCLURE;
         long long ngath = 0;  // texel gathers of this wave for this problem
         while (!st.done) {
             // project, gather, loss (+ partials)
@@ -1132,11 +1165,11 @@ __global__ __launch_bounds__(NT, WPS) void lm_kernel(LaunchArgs a) {
                 if (!ratio_exchange(lmax)) break;
                 contrib_pass(q, mmax);
             }
-            if (st.c.G > 1) team_arrive();
+            if (TEAM) team_arrive();
             else __syncthreads();
-            if (tid < 64 && (st.c.G == 1 || team_wait())) {
+            if (tid < 64 && (!TEAM || team_wait())) {
                 dbg_stamp(q.stamps, 3);  // slowest wave + exchange
-                combine_final_wave(mmax);
+                combine_final_wave(mmax, TEAM);
                 dbg_stamp(q.stamps, 4);
                 lm_update_wave();
             }
@@ -1155,24 +1188,32 @@ __global__ __launch_bounds__(NT, WPS) void lm_kernel(LaunchArgs a) {
             a.stamps[((size_t)blockIdx.x * (NT / 64) + (tid >> 6)) * NSTAMP + k] = st.stamp_ph[tid >> 6][k];
 }
 
-template __global__ void lm_kernel<float, WPS_LATENCY>(LaunchArgs);
-template __global__ void lm_kernel<double, WPS_LATENCY>(LaunchArgs);
-template __global__ void lm_kernel<float, WPS_THROUGHPUT>(LaunchArgs);
-template __global__ void lm_kernel<double, WPS_THROUGHPUT>(LaunchArgs);
-
-hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream) {
-    const bool f32 = dtype == FMPNP_F32, tp = a.wps == WPS_THROUGHPUT;
-    if (f32 && !tp) hipLaunchKernelGGL((lm_kernel<float, WPS_LATENCY>), dim3(grid), dim3(NT), lds, stream, a);
-    else if (f32) hipLaunchKernelGGL((lm_kernel<float, WPS_THROUGHPUT>), dim3(grid), dim3(NT), lds, stream, a);
-    else if (!tp) hipLaunchKernelGGL((lm_kernel<double, WPS_LATENCY>), dim3(grid), dim3(NT), lds, stream, a);
-    else hipLaunchKernelGGL((lm_kernel<double, WPS_THROUGHPUT>), dim3(grid), dim3(NT), lds, stream, a);
-    return hipGetLastError();
+// variant table: [f32][wps == THROUGHPUT][team][ratio][gm] (the throughput variant is only
+// planned with G == 1)
+typedef void (*LmFn)(LaunchArgs);
+template <typename T, int WPS>
+static LmFn lm_pick(bool team, bool ratio, bool gm) {
+    if (team) {
+        if (ratio) return gm ? lm_kernel<T, WPS, true, true, true> : lm_kernel<T, WPS, true, true, false>;
+        return gm ? lm_kernel<T, WPS, true, false, true> : lm_kernel<T, WPS, true, false, false>;
+    }
+    if (ratio) return gm ? lm_kernel<T, WPS, false, true, true> : lm_kernel<T, WPS, false, true, false>;
+    return gm ? lm_kernel<T, WPS, false, false, true> : lm_kernel<T, WPS, false, false, false>;
 }
 
-const void *lm_kernel_ptr(int dtype, int wps) {
+const void *lm_kernel_ptr(int dtype, int wps, bool team, bool ratio, bool gm) {
     const bool f32 = dtype == FMPNP_F32, tp = wps == WPS_THROUGHPUT;
-    if (f32) return tp ? (const void *)lm_kernel<float, WPS_THROUGHPUT> : (const void *)lm_kernel<float, WPS_LATENCY>;
-    return tp ? (const void *)lm_kernel<double, WPS_THROUGHPUT> : (const void *)lm_kernel<double, WPS_LATENCY>;
+    LmFn f;
+    if (f32) f = tp ? lm_pick<float, WPS_THROUGHPUT>(team, ratio, gm) : lm_pick<float, WPS_LATENCY>(team, ratio, gm);
+    else f = tp ? lm_pick<double, WPS_THROUGHPUT>(team, ratio, gm) : lm_pick<double, WPS_LATENCY>(team, ratio, gm);
+    return (const void *)f;
+}
+
+hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream) {
+    const bool gm = a.opt.loss == FMPNP_GEMAN_MCCLURE && a.opt.mode == FMPNP_MODE_FORWARD;
+    const LmFn f = (LmFn)lm_kernel_ptr(dtype, a.wps, a.G > 1, a.opt.use_ratio != 0, gm);
+    hipLaunchKernelGGL(f, dim3(grid), dim3(NT), lds, stream, a);
+    return hipGetLastError();
 }
 
 size_t lm_dyn_lds_bytes(int mmax, int nc_max) {
