@@ -77,6 +77,15 @@ __device__ __forceinline__ double wave_nanmax(double v) {
     return nanmax(a, b);
 }
 
+// 1/x by v_rcp_f64 and two Newton steps (about 0.5 ulp; not always the correctly rounded
+// quotient): used where the reference's division only feeds weights, Jacobians or the
+// mean cost, never a pixel rounding.
+__device__ __forceinline__ double recip(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(fma(-x, r, 1.0), r, r);
+    return fma(fma(-x, r, 1.0), r, r);
+}
+
 // torch.finfo(torch.float).eps as the reference uses it (helpers/utils.py:25,58)
 constexpr double kEpsF32 = 1.1920928955078125e-07;
 
@@ -103,10 +112,10 @@ __device__ __forceinline__ void loss_eval(int loss, double alpha, double x, doub
         d1 = 1.0;
     } else if (alpha == -2.0) {
         // Geman-McClure: beta_safe = 4, alpha_safe = -2 -> rho = -4 (b^-1 - 1), rho' = b^-2 with
-        // b = x/4 + 1.  b^-1 is the correctly rounded 1/b (what a correctly rounded pow returns);
-        // b^-2 as (1/b)^2 is within 2 ulp of pow -- only the weights see it.
+        // b = x/4 + 1.  b^-1 by a Newton-refined reciprocal (within an ulp of pow's correctly
+        // rounded value; rho only enters the mean cost), b^-2 as (1/b)^2.
         const double b = x / 4.0 + 1.0;
-        const double r = 1.0 / b;
+        const double r = recip(b);
         rho = -4.0 * (r - 1.0);
         d1 = r * r;
     } else {                                                            // :58-68

@@ -537,7 +537,7 @@ __device__ __forceinline__ void contrib_block(const PC &q, int mmax, int blk, bo
     const double sxx = kept ? r[3] : 0.0, sxy = kept ? r[4] : 0.0, syy = kept ? r[5] : 0.0;
     // J_px_p (model.py:377-382) times J_p_T (model.py:369-370): A (2x6), A0[1] = A1[0] = 0
     // one reciprocal instead of six divisions (Jacobian entries only: last-bit level)
-    const double iz = 1.0 / z;
+    const double iz = recip(z);
     const double j00 = fx * iz, j02 = ((-fx) * P0 * iz) * iz;
     const double j11 = fy * iz, j12 = ((-fy) * P1 * iz) * iz;
     const double A0[6] = {j00, 0.0, j02, j02 * P1, j00 * z - j02 * P0, -j00 * P1};
@@ -600,9 +600,11 @@ __device__ __forceinline__ void g_issue(GLoad<T> &g, const T *t, const T *rf, in
 }
 // Same accumulation order as gather_half<T, true> (round one, then round two or exact
 // zeros), so both paths give bit-identical sums; has1 = false lanes add nothing.
-template <typename T>
+// FULL: every lane has both rounds (C == 64 V, e.g. C = 256 fp32): no per-lane selects.
+template <typename T, bool FULL>
 __device__ __forceinline__ void g_consume(const GLoad<T> &g, bool has1, bool has2, double a[8]) {
     constexpr int V = V16<T>::n;
+    if (FULL) has1 = has2 = true;
 #pragma unroll
     for (int e = 0; e < 8; ++e) a[e] = 0.0;
     if (!has1) return;
@@ -636,6 +638,45 @@ __device__ __forceinline__ GPair pick_pair(unsigned long long &m, int off, bool 
     return GPair{hi ? b : a, hi ? ob : oa, two};
 }
 
+// Double-buffered pair gathers of one block: the next pair's loads are issued before this
+// pair's channel sums are reduced (one exposed round trip per block, not one per pair).
+// fref0 / rec0: the block's first descriptor row and record.
+template <typename T, bool FULL>
+__device__ __forceinline__ void gather_pipe(unsigned long long m, int off, bool hi, int lane, const T *feat,
+                                            const T *fref0, int cs, int ld, int gc1, int gc2, bool has1, bool has2,
+                                            double *rec0, int e6, bool wlane) {
+    if (!m) return;
+    GLoad<T> A, B;
+    GPair pa = pick_pair(m, off, hi), pb;
+    g_issue<T>(A, feat + (size_t)pa.to * 3 * cs, fref0 + (size_t)pa.j * ld, cs, gc1, gc2);
+    while (true) {
+        const bool moreB = m != 0;
+        if (moreB) {
+            pb = pick_pair(m, off, hi);
+            g_issue<T>(B, feat + (size_t)pb.to * 3 * cs, fref0 + (size_t)pb.j * ld, cs, gc1, gc2);
+        }
+        {
+            double v[8];
+            g_consume<T, FULL>(A, has1, has2, v);
+            const double r = reduce8_in32(v, lane);
+            if (wlane && (!hi || pa.two)) rec0[(size_t)pa.j * RECW + e6] = r;
+        }
+        if (!moreB) break;
+        const bool moreA = m != 0;
+        if (moreA) {
+            pa = pick_pair(m, off, hi);
+            g_issue<T>(A, feat + (size_t)pa.to * 3 * cs, fref0 + (size_t)pa.j * ld, cs, gc1, gc2);
+        }
+        {
+            double v[8];
+            g_consume<T, FULL>(B, has1, has2, v);
+            const double r = reduce8_in32(v, lane);
+            if (wlane && (!hi || pb.two)) rec0[(size_t)pb.j * RECW + e6] = r;
+        }
+        if (!moreA) break;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // One evaluation at (Re, te) over the wave's blocks (no workgroup barrier inside).
 // Without the ratio test each block goes straight on to its chunk partials; with it the
@@ -664,12 +705,13 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
     const bool defer = q.use_ratio != 0;
     double *dst_g = q.part_g;
     if (q.G > 1) dst_g += (size_t)((ufirst((int)st.c.epoch) + 1) & 1) * q.nc_max * NV;
-    // the pose evaluated: uniform, one LDS read per evaluation
+    // the pose evaluated: one LDS broadcast read per evaluation, kept in VGPRs (moving it to
+    // SGPRs costs 24 v_readfirstlane and SGPR spills)
     double Re[9], te[3];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Re[k] = ufirst(st.Re[k]);
+    for (int k = 0; k < 9; ++k) Re[k] = st.Re[k];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) te[k] = ufirst(st.te[k]);
+    for (int k = 0; k < 3; ++k) te[k] = st.te[k];
     double lmax = -1.0;  // -1: nothing supported seen yet
     for (int blk = wave; blk * 64 < M; blk += NT / 64) {
         const int i = blk * 64 + lane;
@@ -702,40 +744,12 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         if (PIPE && onetrip) {
             // double-buffered pairs: the next pair's loads are issued before this pair's
             // channel sums are reduced (one exposed round trip per block, not one per pair)
-            if (m) {
-                GLoad<T> A, B;
-                GPair pa = pick_pair(m, off, hi), pb;
-                g_issue<T>(A, feat + (size_t)pa.to * 3 * cs, fref + (size_t)(p0 + blk * 64 + pa.j) * ld, cs, gc1,
-                           gc2);
-                while (true) {
-                    const bool moreB = m != 0;
-                    if (moreB) {
-                        pb = pick_pair(m, off, hi);
-                        g_issue<T>(B, feat + (size_t)pb.to * 3 * cs, fref + (size_t)(p0 + blk * 64 + pb.j) * ld,
-                                   cs, gc1, gc2);
-                    }
-                    {
-                        double v[8];
-                        g_consume<T>(A, has1, has2, v);
-                        const double r = reduce8_in32(v, lane);
-                        if (wlane && (!hi || pa.two)) rec[(size_t)(blk * 64 + pa.j) * RECW + e6] = r;
-                    }
-                    if (!moreB) break;
-                    const bool moreA = m != 0;
-                    if (moreA) {
-                        pa = pick_pair(m, off, hi);
-                        g_issue<T>(A, feat + (size_t)pa.to * 3 * cs, fref + (size_t)(p0 + blk * 64 + pa.j) * ld,
-                                   cs, gc1, gc2);
-                    }
-                    {
-                        double v[8];
-                        g_consume<T>(B, has1, has2, v);
-                        const double r = reduce8_in32(v, lane);
-                        if (wlane && (!hi || pb.two)) rec[(size_t)(blk * 64 + pb.j) * RECW + e6] = r;
-                    }
-                    if (!moreA) break;
-                }
-            }
+            if (ce - cb == 64 * V)
+                gather_pipe<T, true>(m, off, hi, lane, feat + 0, fref + (size_t)(p0 + blk * 64) * ld, cs, ld, gc1, gc2,
+                                     has1, has2, rec + (size_t)blk * 64 * RECW, e6, wlane);
+            else
+                gather_pipe<T, false>(m, off, hi, lane, feat + 0, fref + (size_t)(p0 + blk * 64) * ld, cs, ld, gc1,
+                                      gc2, has1, has2, rec + (size_t)blk * 64 * RECW, e6, wlane);
         } else {
             while (m) {  // wave-uniform: two dirty points per trip, one per half-wave
                 const GPair pp = pick_pair(m, off, hi);
