@@ -36,6 +36,7 @@
 //     and a second pass over the blocks forms the normal equations.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "fmpnp.h"
@@ -99,11 +100,11 @@ __device__ __forceinline__ P *ufirst(P *p) {
 }
 
 struct LMState {
+    double tot[NV];         // reduced totals of the last evaluation (lane-written by wave 0)
+    double hc[NV];          // cached linearisation at (R, t): H upper triangle, then g
     double R[9], t[3];      // current (last accepted) pose
     double Re[9], te[3];    // pose evaluated next
     double Rb[9], tb[3];    // best pose
-    double Hc[21], gc[6];   // cached linearisation at (R, t)
-    double tot[NV];         // reduced totals of the last evaluation
     double lambda, lr, prev, best, initial, rho_max;
     int best_inl, n_evals, n_steps, n_accepted, status, done, has_best, ret_current;
     int abort_flag, sync_ok;
@@ -851,8 +852,7 @@ __device__ __forceinline__ double combine_final_wave(int mmax, bool team) {
     double a = t, b = t;
     swap32(a, b);  // low half: (own, partner); high half: (partner, own)
     const double tot = a + b;  // even chunks + odd chunks, in both halves
-    if (lane < NV) st.tot[lane] = tot;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back by this wave only
+    if (lane < NV) st.tot[lane] = tot;  // for the solve's broadcast reads
     return tot;
 }
 
@@ -989,19 +989,32 @@ __device__ __forceinline__ bool ldlt_step(const double *Hu, const double *g, dou
 }
 
 // ---------------------------------------------------------------------------
-// LM state machine (model.py:300-486) on wave 0: every lane computes the same uniform
-// state (lane 0 alone writes it back) and the wave solves the 6x6 system together.
-// Every team member computes the same from identical totals.
+// LM state machine (model.py:300-486) on wave 0.  The evaluation's totals arrive
+// lane-distributed (lane j holds value j, from the combine, which also stored them to
+// st.tot); the three the schedule needs are taken by v_readlane.  The scalar state and
+// this lane's pose elements (lane k < 12: R[k] for k < 9, t[k - 9]) are read in one LDS
+// burst; the pose and linearisation copies are lane-wise stores nothing waits on; the
+// solve and the pose update read their uniform operands by LDS broadcast.  Every team
+// member computes the same from identical totals.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void lm_update_wave() {
+__device__ __forceinline__ void lm_update_wave(double tot, bool stamps) {
     LMState &st = S();
     const Ctx &c = st.c;
     const int lane = threadIdx.x & 63;
     const bool w0 = lane == 0;
-    const int nsup = (int)st.tot[29];
-    const int kept = (int)st.tot[28];
-    const double cost = st.tot[27] / st.tot[28];  // torch mean of an empty tensor = NaN
-    if (c.mode == FMPNP_MODE_COMPUTE_COST) {
+    const int kk = lane < 12 ? lane : 0;
+    static_assert(offsetof(LMState, Re) == offsetof(LMState, R) + 12 * sizeof(double), "R/t/Re/te layout");
+    static_assert(offsetof(LMState, hc) == offsetof(LMState, tot) + NV * sizeof(double), "tot/hc layout");
+    // LDS burst: scalar state and this lane's evaluated pose element
+    const double lam_s = st.lambda, lr_s = st.lr, prev = st.prev, best_s = st.best;
+    const int n_evals = st.n_evals, n_steps = st.n_steps;
+    const double pe = st.R[12 + kk];  // [Re | te][k]
+    const int mode = c.mode, n_iters = c.n_iters;
+    const double kept_d = rlane(tot, 28);
+    const int nsup = (int)rlane(tot, 29);
+    const int kept = (int)kept_d;
+    const double cost = rlane(tot, 27) / kept_d;  // torch mean of an empty tensor = NaN
+    if (mode == FMPNP_MODE_COMPUTE_COST) {
         if (w0) {
             st.initial = nsup == 0 ? NAN : cost;
             if (nsup == 0) st.status |= FMPNP_STATUS_NO_SUPPORT;
@@ -1010,7 +1023,6 @@ __device__ __forceinline__ void lm_update_wave() {
         }
         return;
     }
-    const int n_evals = st.n_evals, n_steps = st.n_steps;
     const bool first = n_evals == 0;
     if (nsup == 0) {  // model.py:316-320 / :441-445: return the current pose
         if (w0) {
@@ -1020,10 +1032,9 @@ __device__ __forceinline__ void lm_update_wave() {
         }
         return;
     }
-    double lambda = st.lambda, lr = st.lr;
+    double lambda = lam_s, lr = lr_s;
     bool accepted = true;
     if (!first) {  // model.py:469-478
-        const double prev = st.prev;
         accepted = !(cost > prev);
         const double lam = lambda * (cost > prev ? 10.0 : 0.1);
         lambda = lam < 1e-6 ? 1e-6 : (lam > 1e4 ? 1e4 : lam);
@@ -1036,20 +1047,12 @@ __device__ __forceinline__ void lm_update_wave() {
     }
     // the evaluated pose becomes current and its normal equations the linearisation
     const bool take = first || accepted;
-    const bool new_best = !first && accepted && cost < st.best;
-    // pose / linearisation copies: one element per lane
-    if (new_best && lane < 12) {
-        if (lane < 9) st.Rb[lane] = st.Re[lane];
-        else st.tb[lane - 9] = st.te[lane - 9];
+    const bool new_best = !first && accepted && cost < best_s;
+    if (lane < 12) {
+        if (new_best) st.Rb[lane] = pe;  // [Rb | tb] contiguous
+        if (take) st.R[lane] = pe;       // [R | t]
     }
-    if (take && lane < 12) {
-        if (lane < 9) st.R[lane] = st.Re[lane];
-        else st.t[lane - 9] = st.te[lane - 9];
-    }
-    if (take && lane < 27) {
-        if (lane < 21) st.Hc[lane] = st.tot[lane];
-        else st.gc[lane - 21] = st.tot[lane];
-    }
+    if (take && lane < NV) st.hc[lane] = tot;
     if (w0) {
         if (first) {  // model.py:347-359
             st.prev = st.best = st.initial = cost;
@@ -1065,10 +1068,13 @@ __device__ __forceinline__ void lm_update_wave() {
         }
         st.lambda = lambda;
         st.lr = lr;
-        if (c.trace && c.s == 0 && n_evals < c.trace_stride) {
-            fmpnp_trace_entry &e = c.trace[(size_t)c.p * c.trace_stride + n_evals];
-            for (int k = 0; k < 9; ++k) e.R[k] = st.Re[k];
-            for (int k = 0; k < 3; ++k) e.t[k] = st.te[k];
+        st.n_evals = n_evals + 1;
+    }
+    if (c.trace && c.s == 0 && n_evals < c.trace_stride) {
+        fmpnp_trace_entry &e = c.trace[(size_t)c.p * c.trace_stride + n_evals];
+        if (lane < 9) e.R[lane] = pe;
+        else if (lane < 12) e.t[lane - 9] = pe;
+        if (w0) {
             e.cost = cost;
             e.lambda_after = lambda;
             e.lr_after = lr;
@@ -1076,20 +1082,23 @@ __device__ __forceinline__ void lm_update_wave() {
             e.n_kept = kept;
             e.accepted = accepted ? 1 : 0;
         }
-        st.n_evals = n_evals + 1;
     }
-    if (n_steps >= c.n_iters) {
+    if (n_steps >= n_iters) {
         if (w0) st.done = 1;
         return;
     }
-    // next step from the linearisation at the current pose (model.py:408-426)
-    double delta[6];
-    dbg_stamp(c.stamps_on != 0, 5);  // LM bookkeeping
-    {
-        const double *Hu = take ? st.tot : st.Hc, *gv = take ? st.tot + 21 : st.gc;
-        if (!ldlt_step(Hu, gv, lambda, lr, delta)) lm_step_rows(Hu, gv, lambda, lr, delta);
-    }
-    dbg_stamp(c.stamps_on != 0, 6);  // 6x6 solve
+    // next step from the linearisation at the current pose (model.py:408-426); uniform
+    // operands by LDS broadcast (this wave's own stores above: LDS is in order per wave)
+    const double *hs = st.tot + (take ? 0 : NV);
+    double Hu[21], gv[6], delta[6];
+#pragma unroll
+    for (int k = 0; k < 21; ++k) Hu[k] = hs[k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) gv[k] = hs[21 + k];
+    dbg_stamp(stamps, 5);  // LM bookkeeping
+    // (the pivoted-LU fallback indexes H by lane: it reads the LDS copy, not a private array)
+    if (!ldlt_step(Hu, gv, lambda, lr, delta)) lm_step_rows(hs, hs + 21, lambda, lr, delta);
+    dbg_stamp(stamps, 6);  // 6x6 solve
     bool bad = false;
 #pragma unroll
     for (int k = 0; k < 6; ++k) bad |= isnan(delta[k]);
@@ -1101,13 +1110,12 @@ __device__ __forceinline__ void lm_update_wave() {
         }
         return;
     }
-    const double *R = take ? st.Re : st.R;
-    const double *t = take ? st.te : st.t;
+    const double *pp = st.R + (take ? 12 : 0);  // [R | t] or [Re | te]
     double Rc[9], tc[3], Rn[9], tn[3];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Rc[k] = R[k];
+    for (int k = 0; k < 9; ++k) Rc[k] = pp[k];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) tc[k] = t[k];
+    for (int k = 0; k < 3; ++k) tc[k] = pp[9 + k];
     pose_update(Rc, tc, delta, Rn, tn);
     if (w0) {
         st.n_steps = n_steps + 1;
@@ -1183,9 +1191,9 @@ __global__ __launch_bounds__(NT, WPS) void lm_kernel(LaunchArgs a) {
             else __syncthreads();
             if (tid < 64 && (!TEAM || team_wait())) {
                 dbg_stamp(q.stamps, 3);  // slowest wave + exchange
-                combine_final_wave(mmax, TEAM);
+                const double tot = combine_final_wave(mmax, TEAM);
                 dbg_stamp(q.stamps, 4);
-                lm_update_wave();
+                lm_update_wave(tot, q.stamps);
             }
             __syncthreads();
             dbg_stamp(q.stamps, 7);  // pose update + barrier
