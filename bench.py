@@ -170,7 +170,7 @@ def main():
         extras = run_extras(args, dev, probs, keep, opts, rf, _lib, synth)
 
     if rank == 0:
-        traffic = load_traffic(B)
+        traffic, traffic_kernel = load_traffic(B)
         out = {
             "metric": "pose-refinements/sec (N=512 pts, C=256, 240x320, 50 LM iters)",
             "value": round(value, 3),
@@ -195,7 +195,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
                          "traffic": traffic,
-                         "kernel": "fmpnp::lm_kernel<float>", "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
+                         "kernel": traffic_kernel or "fmpnp::lm_kernel<float, 2, false, false, true>",
+                         "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "bytes_rule": "SURVEY.md 8d: B * iters * N*(16C+24) (f, gx, gy, fref fp32 at one "
                                        "texel + fp64 point per GN iteration)",
@@ -217,16 +218,18 @@ def main():
 
 
 def load_traffic(B):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this workload, if any."""
+    """(HBM bytes per launch, kernel name) from the committed rocprofv3 PMC summary of this
+    workload (profiles/pmc_traffic.json, tools/gpu_profile.sh), if any."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
         if d.get("batch") == B:
-            return d.get("hbm_bytes_per_launch")
+            name = (d.get("kernel") or "").replace("void ", "").replace("(fmpnp::LaunchArgs)", "")
+            return d.get("hbm_bytes_per_launch"), name or None
     except (OSError, ValueError):
         pass
-    return None
+    return None, None
 
 
 def run_extras(args, dev, probs, keep, opts, rf, _lib, synth):

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -107,9 +108,13 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     P.G = G;
     P.mmax = ((P.nc_max + G - 1) / G) * CH;
     P.lds = lds_for(G);
-    // two workgroups per CU once there are enough single-workgroup problems to fill them
-    // (measured B=512: 1.11 -> 0.99 ms); below that the 256-VGPR variant is faster
-    P.wps = (G == 1 && (long)n >= 2L * ncu && 2 * P.lds <= lds_cu) ? WPS_THROUGHPUT : WPS_LATENCY;
+    // occupancy variant: the 128-VGPR two-workgroups-per-CU build (WPS_THROUGHPUT) spills
+    // since the kernel went register-resident (73-106 VGPRs to scratch) and measured slower
+    // than running the latency build in rounds (B=512: 0.93 ms vs 2 x 0.42 ms), so the
+    // planner uses it only on request (FMPNP_LM_WPS=4, a tuning knob)
+    const char *wps_env = getenv("FMPNP_LM_WPS");
+    const bool want_tp = wps_env && atoi(wps_env) == 4;
+    P.wps = (want_tp && G == 1 && (long)n >= 2L * ncu && 2 * P.lds <= lds_cu) ? WPS_THROUGHPUT : WPS_LATENCY;
     const int per_cu = occupancy(P.lds);
     long cap = (long)ncu * per_cu;
     if (G == 1) cap = std::max(cap, (long)n);  // no cross-workgroup waits: any grid is safe

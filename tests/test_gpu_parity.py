@@ -138,9 +138,12 @@ def test_batch_equals_individual():
         assert r1["status"] == rb["status"]
 
 
-def test_large_batch_throughput_variant_equals_individual():
-    """n >= 2 x CUs selects the two-workgroups-per-CU kernel (128 VGPRs): its results must be
-    bit-identical to single-problem launches (which use the 256-VGPR kernel)."""
+@pytest.mark.parametrize("wps", ["2", "4"])
+def test_large_batch_throughput_variant_equals_individual(wps, monkeypatch):
+    """n >= 2 x CUs: the problems run in rounds of resident teams (default) or, with
+    FMPNP_LM_WPS=4, on the two-workgroups-per-CU kernel (128 VGPRs); either way the results
+    must be bit-identical to single-problem launches (the 256-VGPR kernel)."""
+    monkeypatch.setenv("FMPNP_LM_WPS", wps)
     names = ["gm_c16", "behind_camera_gm", "odd_geom_gm", "no_support_init", "ratio08_gm"]
     base = []
     for nm in names:
