@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-extras", action="store_true", help="skip single-query / pack / CPU legs")
     ap.add_argument("--no-nomemo", action="store_true", help="skip the memoisation-off comparison launch")
+    ap.add_argument("--no-bilinear", action="store_true", help="skip the bilinear-sampling launch")
     return ap.parse_args()
 
 
@@ -165,6 +166,35 @@ def main():
               "frac": round(nm_bytes / nm_s / HBM_PEAK, 4), "poses_bit_identical_to_memoised": bool(same)}
         del batch_nm
 
+    # bilinear sampling (extension, FMPNP_BILINEAR): every supported point reads its 2x2 taps
+    # of f, gx, gy plus fref at every evaluation -- SURVEY.md 8d's N*(52C+24) bytes per GN
+    # iteration, no memoisation: the bandwidth-bound form of the loop
+    bil = {}
+    if not args.no_bilinear:
+        opts_b = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32, wgs_per_problem=args.wgs,
+                                 sampling="bilinear")
+        batch_b = rf.AsyncBatch(probs, opts_b)
+        batch_b.launch()
+        torch.cuda.synchronize()
+        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = max(1, min(args.steps, 3))
+        s_ev.record(stream)
+        for _ in range(reps):
+            batch_b.launch()
+        e_ev.record(stream)
+        torch.cuda.synchronize()
+        b_s = s_ev.elapsed_time(e_ev) / reps / 1e3
+        res_b = batch_b.results()
+        b_evals = int(sum(r["n_evals"] for r in res_b))
+        b_bytes = b_evals * N_PTS * (52 * C + 24)  # every evaluation samples every point (upper bound)
+        bil = {"ms_per_launch": round(b_s * 1e3, 4), "pose_refinements_per_s": round(B / b_s, 1),
+               "gn_iters_per_s": round(B * ITERS / b_s, 1), "algorithmic_bytes_per_launch": b_bytes,
+               "bytes_rule": "SURVEY.md 8d bilinear: N*(52C+24) per point-evaluation (4 taps x f,gx,gy + fref "
+                             "fp32, fp64 point)",
+               "achieved_GB_per_s": round(b_bytes / b_s / 1e9, 1), "frac": round(b_bytes / b_s / HBM_PEAK, 4),
+               "statuses": sorted({r["status"] for r in res_b})}
+        del batch_b
+
     extras = {}
     if rank == 0 and not args.no_extras:
         extras = run_extras(args, dev, probs, keep, opts, rf, _lib, synth)
@@ -208,6 +238,7 @@ def main():
                                  "peak is possible; gathered_* is what it actually reads, no_memo the "
                                  "HBM-bound form"},
             "no_memo": nm,
+            "bilinear": bil,
             "statuses": statuses,
         }
         out.update(extras)

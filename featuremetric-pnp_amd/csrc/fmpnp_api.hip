@@ -38,7 +38,7 @@ int validate(const fmpnp_problem *probs, int n, const fmpnp_options *opt) {
     if (opt->dtype != FMPNP_F32 && opt->dtype != FMPNP_F64) return FMPNP_EINVAL;
     if (opt->loss < FMPNP_SQUARED || opt->loss > FMPNP_BARRON) return FMPNP_EINVAL;
     if (opt->mode != FMPNP_MODE_FORWARD && opt->mode != FMPNP_MODE_COMPUTE_COST) return FMPNP_EINVAL;
-    if (opt->sampling != FMPNP_NEAREST) return FMPNP_EINVAL;  // bilinear: not in this build
+    if (opt->sampling != FMPNP_NEAREST && opt->sampling != FMPNP_BILINEAR) return FMPNP_EINVAL;
     for (int i = 0; i < n; ++i) {
         const fmpnp_problem &p = probs[i];
         if (p.N < 0 || p.Hf <= 0 || p.Wf <= 0 || p.im_width <= 0 || p.im_height <= 0) return FMPNP_EINVAL;
@@ -82,8 +82,9 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     // (MI355X_MICROARCH.md, Residency) -> min(api, 6).
     auto occupancy = [&](int lds) {
         int nb = 0;
-        const bool gm = opt->loss == FMPNP_GEMAN_MCCLURE && opt->mode == FMPNP_MODE_FORWARD;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lm_kernel_ptr(opt->dtype, P.wps, P.G > 1, opt->use_ratio != 0, gm),
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb,
+                                                         lm_kernel_ptr(opt->dtype, P.wps, P.G > 1,
+                                                                       opt->use_ratio != 0, lm_variant(*opt)),
                                                          NT, lds) !=
             hipSuccess)
             return 1;

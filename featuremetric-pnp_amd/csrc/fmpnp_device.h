@@ -163,8 +163,10 @@ __device__ __forceinline__ void transform_pt(const double *R, const double *t, d
 }
 
 // Pixel of a camera-frame point: round_half_even(K P / P_z) - 1 and the image mask
-// (model.py:306-311, points_within_image :99-117; z<0 is NOT masked).
-__device__ __forceinline__ bool project_px(const double *K, const double P[3], int W, int H, int &x, int &y) {
+// (model.py:306-311, points_within_image :99-117; z<0 is NOT masked).  qx, qy: the
+// unrounded K P / P_z (bilinear sampling).
+__device__ __forceinline__ bool project_px(const double *K, const double P[3], int W, int H, int &x, int &y,
+                                          double &qx, double &qy) {
 #pragma clang fp contract(off)
     double u[3];
     for (int i = 0; i < 3; ++i) {
@@ -173,12 +175,56 @@ __device__ __forceinline__ bool project_px(const double *K, const double P[3], i
         s = s + K[3 * i + 2] * P[2];
         u[i] = s;
     }
-    double px = rint(u[0] / u[2]) - 1.0;
-    double py = rint(u[1] / u[2]) - 1.0;
+    qx = u[0] / u[2];
+    qy = u[1] / u[2];
+    double px = rint(qx) - 1.0;
+    double py = rint(qy) - 1.0;
     if (!(px >= 0.0 && px < (double)W && py >= 0.0 && py < (double)H)) return false;
     x = (int)px;
     y = (int)py;
     return true;
+}
+
+// Bilinear sampling (FMPNP_BILINEAR, an extension: the reference's indexing_ is
+// nearest-texel).  The definition is shared bit-for-bit with the oracle
+// (oracle/fmpnp_oracle.c bilinear_taps): sx = ((qx - 0.5) Wf) / W - 0.5 (image pixel
+// index i = round(q) - 1 is centred at q = i + 1, texel c at sx = c), taps at
+// floor(sx), floor(sx) + 1 (rows likewise) clamped to the map, weights
+// w00 = (1-ax)(1-ay), w01 = ax(1-ay), w10 = (1-ax)ay, w11 = ax ay.
+struct Taps {
+    int off[4];       // texel offsets (row * Wf + col): [y0x0, y0x1, y1x0, y1x1]
+    double w[4];
+};
+__device__ __forceinline__ void bilinear_taps(double qx, double qy, int Hf, int Wf, int W, int H, Taps &t) {
+#pragma clang fp contract(off)
+    const double sx = ((qx - 0.5) * (double)Wf) / (double)W - 0.5;
+    const double sy = ((qy - 0.5) * (double)Hf) / (double)H - 0.5;
+    const double fx0 = floor(sx), fy0 = floor(sy);
+    const double ax = sx - fx0, ay = sy - fy0;
+    int x0 = (int)fx0, y0 = (int)fy0, x1 = x0 + 1, y1 = y0 + 1;
+    x0 = min(max(x0, 0), Wf - 1);
+    x1 = min(max(x1, 0), Wf - 1);
+    y0 = min(max(y0, 0), Hf - 1);
+    y1 = min(max(y1, 0), Hf - 1);
+    t.off[0] = y0 * Wf + x0;
+    t.off[1] = y0 * Wf + x1;
+    t.off[2] = y1 * Wf + x0;
+    t.off[3] = y1 * Wf + x1;
+    t.w[0] = (1.0 - ax) * (1.0 - ay);
+    t.w[1] = ax * (1.0 - ay);
+    t.w[2] = (1.0 - ax) * ay;
+    t.w[3] = ax * ay;
+}
+// one sampled value: fma(w11, v11, fma(w10, v10, fma(w01, v01, w00 v00)))
+__device__ __forceinline__ double sample4(const double w[4], double v0, double v1, double v2, double v3) {
+    return fma(w[3], v3, fma(w[2], v2, fma(w[1], v1, w[0] * v0)));
+}
+
+__device__ __forceinline__ double rlane64(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
 }  // namespace fmpnp

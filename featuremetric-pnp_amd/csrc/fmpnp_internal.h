@@ -40,7 +40,11 @@ __host__ __device__ constexpr int lds_fixed_bytes() { return 4096; }
 size_t lm_dyn_lds_bytes(int mmax, int nc_max);
 
 hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream);
-const void *lm_kernel_ptr(int dtype, int wps, bool team, bool ratio, bool gm);
+// LM kernel variants (fmpnp_lm_impl.h): Geman-McClure forward with nearest sampling (the
+// hot path), any loss / mode with nearest sampling, bilinear sampling
+constexpr int VAR_NEAREST = 0, VAR_GM = 1, VAR_BILINEAR = 2;
+int lm_variant(const fmpnp_options &o);
+const void *lm_kernel_ptr(int dtype, int wps, bool team, bool ratio, int var);
 
 hipError_t launch_pack(const void *chw, const void *gx, const void *gy, int dtype_in, int C, int H, int W, void *out,
                        int dtype_out, int cstride, int normalized, int replicate, hipStream_t stream);

@@ -1,0 +1,27 @@
+// fmpnp_lm_f64.hip -- LM kernel variants for double texels (see fmpnp_lm_impl.h).  One
+// translation unit per storage type, so the variants compile in parallel.
+#include "fmpnp_lm_impl.h"
+
+namespace fmpnp {
+
+typedef void (*LmFn)(LaunchArgs);
+template <int WPS, bool TEAM, bool RATIO>
+static LmFn pick_var(int var) {
+    if (var == VAR_GM) return lm_kernel<double, WPS, TEAM, RATIO, VAR_GM>;
+    if (var == VAR_BILINEAR) return lm_kernel<double, WPS, TEAM, RATIO, VAR_BILINEAR>;
+    return lm_kernel<double, WPS, TEAM, RATIO, VAR_NEAREST>;
+}
+template <int WPS>
+static LmFn pick(bool team, bool ratio, int var) {
+    if (team) return ratio ? pick_var<WPS, true, true>(var) : pick_var<WPS, true, false>(var);
+    return ratio ? pick_var<WPS, false, true>(var) : pick_var<WPS, false, false>(var);
+}
+
+const void *lm_kernel_ptr_f64(int wps, bool team, bool ratio, int var) {
+    // the 128-VGPR throughput build is only planned with G == 1
+    if (wps == WPS_THROUGHPUT) return (const void *)(ratio ? pick_var<WPS_THROUGHPUT, false, true>(var)
+                                                           : pick_var<WPS_THROUGHPUT, false, false>(var));
+    return (const void *)pick<WPS_LATENCY>(team, ratio, var);
+}
+
+}  // namespace fmpnp

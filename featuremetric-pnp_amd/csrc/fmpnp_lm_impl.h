@@ -1,0 +1,1311 @@
+// fmpnp_lm_impl.h -- the LM kernel template (included by the per-storage-type
+// instantiation units fmpnp_lm_f32.hip / fmpnp_lm_f64.hip).
+#pragma once
+// fmpnp_lm.hip -- the feature-metric LM refiner on gfx950 (MI355X).
+//
+// One launch runs the WHOLE Levenberg-Marquardt loop of every problem of a batch
+// (sparseFeaturePnP.forward, featurePnP/model.py:245-494) on the device.
+//
+// Work decomposition
+//   * A "team" of G workgroups (512 threads = 8 waves each) owns one problem at a time;
+//     teams walk the batch persistently (problem = team, team + T, ...).
+//   * Points are cut into chunks of CH = 16; workgroup s of a team owns a contiguous
+//     range of chunks, and wave w of the workgroup owns the 64-point blocks w, w+8, ...
+//     of that range.  Per evaluation a wave carries each of its blocks from projection
+//     to chunk partials with NO workgroup barrier:
+//       project  (lane per point, fp64, exact pixel rounding) -> texel offset, P;
+//       gather   the points whose texel changed (ballot), two per wave: each half-wave
+//                issues 16-byte loads of the channels-last [H][W][3][C] texel and fref
+//                and reduces the six channel sums  sum e^2, sum gx e, sum gy e, sum gx^2,
+//                sum gx gy, sum gy^2  in fp64 (the C x 6 Jacobian is never materialised:
+//                J = G A with the 2x6 pose chain A, so J^T e = A^T (G^T e),
+//                J^T J = A^T (G^T G) A); unchanged texels keep their sums (memoisation);
+//       loss + normal equations (lane per point) -> 21 + 6 entries, rho and counters,
+//                reduced per 16-point chunk by a fixed transposed DPP tree.
+//   * The chunk partials are summed by wave 0 with a fixed tree over CHUNK INDICES.  Results
+//     are therefore deterministic and independent of G: the LM accept test `new > prev`
+//     (model.py:469-472) compares costs that tie exactly whenever the pixel sets are
+//     equal, and a scheduling-dependent sum would break those ties.
+//   * G > 1: chunk partials go to a per-team slot with write-through (sc1) stores,
+//     every storing wave drains, one lane bumps the team's arrival counter, one lane
+//     polls it (bounded spin), one agent-scope acquire; then wave 0 of every member
+//     reads all partials and runs the identical 6x6 solve + LM update (no second exchange).
+//   * One evaluation per iteration: the trial evaluation at (R', t') also produces that
+//     pose's normal equations.  On acceptance they are the next linearisation; on
+//     rejection the cached ones are reused -- bit-identical to the reference's
+//     recomputation at the unchanged pose (model.py:472-476).
+//   * The ratio test (model.py:324-336) needs max|rho| over the team before any point's
+//     weight is known: with it, loss values are parked in LDS, the maximum is exchanged,
+//     and a second pass over the blocks forms the normal equations.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "fmpnp.h"
+#include "fmpnp_device.h"
+#include "fmpnp_internal.h"
+
+namespace fmpnp {
+
+// dynamic LDS of the LM kernel (the only kernel in this file that uses LDS)
+extern __shared__ __attribute__((aligned(16))) unsigned char lm_lds[];
+
+struct Ctx {
+    // launch constants
+    fmpnp_result *results;
+    fmpnp_trace_entry *trace;
+    unsigned *counter;
+    double *part_g;       // [2][nc_max][NV] of this team
+    double *max_g;        // [2][G] of this team
+    double lambda0, ratio_thr, alpha;
+    int mode, n_iters, use_ratio, loss, G, s, trace_stride, nc_max, no_memo, sampling;
+    unsigned epoch;       // exchanges done by this team in this launch
+    int dead;             // a team exchange timed out: finish remaining problems as failed
+    int stamps_on;        // debug phase stamps enabled
+    // problem constants
+    const void *feat;
+    const void *fref;
+    const double *pts;
+    double K[9];
+    int p, N, Hf, Wf, cs, cb, ce, ld_ref, im_w, im_h, vec;
+    UDiv div_h, div_w;    // exact floor division by im_h, im_w (indexing_)
+    int p0, M, c0, LC, NC;
+};
+
+// Per-problem constants of the point phases, held in registers (every value wave-uniform:
+// the compiler keeps them in SGPRs) instead of being re-read from the LDS Ctx at every use
+// -- each LDS read is a ~100-cycle round trip on the evaluation's critical path.
+struct PC {
+    const void *feat, *fref;
+    double K[9];
+    int Hf, Wf, cs, cb, ce, ld, im_w, im_h, p0, M, c0, LC, G;
+    UDiv dh, dw;
+    int loss, no_memo, use_ratio, bilinear;
+    double alpha;
+    double *part_g;       // this team's partial slots [2][nc_max][NV] (G > 1)
+    int nc_max;
+    bool stamps;          // debug phase stamps on
+};
+
+__device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ unsigned ufirst(unsigned v) { return (unsigned)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ double ufirst(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <typename P>
+__device__ __forceinline__ P *ufirst(P *p) {
+    const uintptr_t b = (uintptr_t)p;
+    const unsigned lo = ufirst((unsigned)b), hi = ufirst((unsigned)(b >> 32));
+    return (P *)(((uintptr_t)hi << 32) | lo);
+}
+
+struct LMState {
+    double tot[NV];         // reduced totals of the last evaluation (lane-written by wave 0)
+    double hc[NV];          // cached linearisation at (R, t): H upper triangle, then g
+    double R[9], t[3];      // current (last accepted) pose
+    double Re[9], te[3];    // pose evaluated next
+    double Rb[9], tb[3];    // best pose
+    double lambda, lr, prev, best, initial, rho_max;
+    int best_inl, n_evals, n_steps, n_accepted, status, done, has_best, ret_current;
+    int abort_flag, sync_ok;
+    double wg_max[NT / 64];
+    unsigned long long stamp_t[NT / 64], stamp_ph[NT / 64][NSTAMP];  // debug phase stamps (lane 0 per wave)
+    Ctx c;
+};
+static_assert(sizeof(LMState) <= lds_fixed_bytes(), "LDS head too small");
+
+__device__ __forceinline__ LMState &S() { return *reinterpret_cast<LMState *>(lm_lds); }
+
+// Registers <- the LDS Ctx, once per problem (after problem_begin's barrier).
+__device__ __forceinline__ PC load_pc() {
+    const Ctx &c = S().c;
+    PC q;
+    q.feat = ufirst(c.feat);
+    q.fref = ufirst(c.fref);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) q.K[k] = ufirst(c.K[k]);
+    q.Hf = ufirst(c.Hf); q.Wf = ufirst(c.Wf); q.cs = ufirst(c.cs); q.cb = ufirst(c.cb); q.ce = ufirst(c.ce);
+    q.ld = ufirst(c.ld_ref); q.im_w = ufirst(c.im_w); q.im_h = ufirst(c.im_h); q.p0 = ufirst(c.p0);
+    q.M = ufirst(c.M); q.c0 = ufirst(c.c0); q.LC = ufirst(c.LC); q.G = ufirst(c.G);
+    q.dh = UDiv{ufirst(c.div_h.m), ufirst(c.div_h.s1), ufirst(c.div_h.s2)};
+    q.dw = UDiv{ufirst(c.div_w.m), ufirst(c.div_w.s1), ufirst(c.div_w.s2)};
+    q.loss = ufirst(c.mode == FMPNP_MODE_COMPUTE_COST ? (int)FMPNP_SQUARED : c.loss);
+    q.no_memo = ufirst(c.no_memo);
+    q.bilinear = ufirst(c.sampling == FMPNP_BILINEAR ? 1 : 0);
+    q.use_ratio = ufirst(c.use_ratio);
+    q.alpha = ufirst(c.alpha);
+    q.part_g = ufirst(c.part_g);
+    q.nc_max = ufirst(c.nc_max);
+    q.stamps = ufirst(c.stamps_on) != 0;
+    return q;
+}
+// debug: add the cycles since the wave's previous stamp to its phase k (lane 0 of each
+// wave); phases 0..3 of the first evaluation go to slots 8..11
+__device__ __forceinline__ void dbg_stamp(bool on, int k) {
+    LMState &st = *reinterpret_cast<LMState *>(lm_lds);
+    if (on && (threadIdx.x & 63) == 0) {
+        const int w = threadIdx.x >> 6;
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        st.stamp_ph[w][k < 4 && st.n_evals == 0 ? 8 + k : k] += now - st.stamp_t[w];
+        st.stamp_t[w] = now;
+    }
+}
+__device__ __forceinline__ unsigned char *dyn() { return lm_lds + lds_fixed_bytes(); }
+// dynamic carve (mmax = max local points, a multiple of CH):
+//   X[mmax][3], rec[mmax][RECW] doubles, tex[mmax] ints (16-B padded), part[nc_max][NV] doubles
+__device__ __forceinline__ double *lds_X(int mmax) { return reinterpret_cast<double *>(dyn()); }
+__device__ __forceinline__ double *lds_rec(int mmax) { return reinterpret_cast<double *>(dyn()) + 3 * mmax; }
+__device__ __forceinline__ int *lds_tex(int mmax) {
+    return reinterpret_cast<int *>(reinterpret_cast<double *>(dyn()) + (3 + RECW) * mmax);
+}
+__device__ __forceinline__ double *lds_part(int mmax) {
+    return reinterpret_cast<double *>(dyn()) + (3 + RECW) * mmax + ((mmax + 3) / 4) * 2;
+}
+
+// sin, cos of 0 <= x <= pi/4 by Horner-form Taylor series to x^17 / x^18 (truncation
+// below 1e-19 relative; a few ulp of rounding): ~20 register-resident fp64 operations
+// instead of the library's range-reduced sincos on the LM tail's critical path.
+__device__ __forceinline__ void sincos_small(double x, double &s, double &c) {
+    const double z = x * x;
+    double ps = 1.0 / 355687428096000.0;
+    ps = fma(ps, z, -1.0 / 1307674368000.0);
+    ps = fma(ps, z, 1.0 / 6227020800.0);
+    ps = fma(ps, z, -1.0 / 39916800.0);
+    ps = fma(ps, z, 1.0 / 362880.0);
+    ps = fma(ps, z, -1.0 / 5040.0);
+    ps = fma(ps, z, 1.0 / 120.0);
+    ps = fma(ps, z, -1.0 / 6.0);
+    s = fma(x * z, ps, x);
+    double pc = -1.0 / 6402373705728000.0;
+    pc = fma(pc, z, 1.0 / 20922789888000.0);
+    pc = fma(pc, z, -1.0 / 87178291200.0);
+    pc = fma(pc, z, 1.0 / 479001600.0);
+    pc = fma(pc, z, -1.0 / 3628800.0);
+    pc = fma(pc, z, 1.0 / 40320.0);
+    pc = fma(pc, z, -1.0 / 720.0);
+    pc = fma(pc, z, 1.0 / 24.0);
+    pc = fma(pc, z, -0.5);
+    c = fma(z, pc, 1.0);
+}
+
+// so3exp_map (helpers/utils.py:209-221) and the update R' = dR R, t' = dR t + dt
+// (model.py:416-426).
+__device__ __forceinline__ void pose_update(const double *R, const double *t, const double delta[6], double *Rn,
+                                            double *tn) {
+    const double w0 = delta[3], w1 = delta[4], w2 = delta[5];
+    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+    double dR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    if (isnan(theta)) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) dR[i] = NAN;
+    } else if (!(theta < 1e-12)) {
+        const double it = 1.0 / theta;  // w / theta within 1 ulp, one division instead of three
+        const double k0 = w0 * it, k1 = w1 * it, k2 = w2 * it;
+        const double W[9] = {0, -k2, k1, k2, 0, -k0, -k1, k0, 0};
+        double s, c;
+        if (theta <= 0.78539816339744828) sincos_small(theta, s, c);
+        else sincos(theta, &s, &c);
+        const double c1 = 1.0 - c;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                double ww = W[3 * i + 0] * W[0 + j] + W[3 * i + 1] * W[3 + j] + W[3 * i + 2] * W[6 + j];
+                dR[3 * i + j] += W[3 * i + j] * s + ww * c1;
+            }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            Rn[3 * i + j] = dR[3 * i + 0] * R[j] + dR[3 * i + 1] * R[3 + j] + dR[3 * i + 2] * R[6 + j];
+        tn[i] = (dR[3 * i + 0] * t[0] + dR[3 * i + 1] * t[1] + dR[3 * i + 2] * t[2]) + delta[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Cross-workgroup exchange inside a team (G > 1), MI355X_MICROARCH.md "sc1 loads in place
+// of the acquire", first row: every byte handed off is stored write-through (sc1) and
+// read back with global sc1 loads; every storing wave drains (vmcnt(0)) before a workgroup
+// barrier, behind which ONE lane per workgroup adds to the team's arrival counter (agent
+// scope); the consumer is the polling wave itself (wave 0), which loads only after its
+// poll has matched -- no L1 invalidate, no second barrier.  The counter is monotonic
+// within a launch and zeroed by the launcher (hipMemsetAsync) before every launch.
+// One workgroup per CU (the planner's launch bounds), memory from hipMalloc.
+// ---------------------------------------------------------------------------
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+typedef __attribute__((address_space(1))) unsigned g_u32;
+#else
+typedef unsigned long long g_u64;  // host pass: never executed
+typedef unsigned g_u32;
+#endif
+__device__ __forceinline__ void st_sc1(double *p, double v) {
+    __hip_atomic_store(reinterpret_cast<g_u64 *>(reinterpret_cast<uintptr_t>(p)), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double *p) {
+    return __longlong_as_double((long long)__hip_atomic_load(
+        reinterpret_cast<g_u64 *>(reinterpret_cast<uintptr_t>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Every thread calls this after its sc1 stores: this workgroup's arrival for the next epoch.
+__device__ __forceinline__ void team_arrive() {
+    LMState &st = S();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ++st.c.epoch;
+        __hip_atomic_fetch_add(reinterpret_cast<g_u32 *>(reinterpret_cast<uintptr_t>(st.c.counter)), 1u,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Wave 0 (all its lanes) after team_arrive: thread 0 polls until every member has arrived
+// for the current epoch (bounded: ~2 s of wall time, s_memrealtime ticks at 100 MHz).
+// Returns false -- and raises the workgroup's abort flag -- on timeout.
+__device__ __forceinline__ bool team_wait() {
+    LMState &st = S();
+    int ok = 1;
+    if (threadIdx.x == 0) {
+        const unsigned target = st.c.epoch * (unsigned)st.c.G;
+        g_u32 *counter = reinterpret_cast<g_u32 *>(reinterpret_cast<uintptr_t>(st.c.counter));
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) { ok = 0; break; }
+        }
+        if (!ok) st.abort_flag = 1;
+    }
+    return __builtin_amdgcn_readfirstlane(ok) != 0;
+}
+
+// ---------------------------------------------------------------------------
+// problem begin / end
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, int mmax) {
+    LMState &st = S();
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        Ctx &c = st.c;
+        c.p = p;
+        c.feat = pb->feat;
+        c.fref = pb->fref;
+        c.pts = pb->pts3d;
+        c.N = pb->N;
+        c.Hf = pb->Hf;
+        c.Wf = pb->Wf;
+        c.cs = pb->cstride;
+        c.cb = pb->c_begin;
+        c.ce = pb->c_end;
+        c.ld_ref = pb->ld_ref;
+        c.im_w = pb->im_width;
+        c.im_h = pb->im_height;
+        for (int k = 0; k < 9; ++k) c.K[k] = pb->K[k];
+        c.div_h = udiv_make((unsigned)c.im_h);
+        c.div_w = udiv_make((unsigned)c.im_w);
+        c.NC = (c.N + CH - 1) / CH;
+        c.c0 = (int)(((long)c.NC * c.s) / c.G);
+        const int c1 = (int)(((long)c.NC * (c.s + 1)) / c.G);
+        c.LC = c1 - c.c0;
+        c.p0 = c.c0 * CH;
+        c.M = max(min(c1 * CH, c.N) - c.p0, 0);
+        c.vec = 0;
+        for (int k = 0; k < 9; ++k) { st.R[k] = st.Re[k] = st.Rb[k] = pb->R0[k]; }
+        for (int k = 0; k < 3; ++k) { st.t[k] = st.te[k] = st.tb[k] = pb->t0[k]; }
+        st.lambda = c.lambda0;
+        st.lr = 1.0;
+        st.prev = st.best = st.initial = NAN;
+        st.best_inl = -1;
+        st.n_evals = st.n_steps = st.n_accepted = 0;
+        st.status = c.dead ? FMPNP_STATUS_SYNC_TIMEOUT : 0;
+        st.has_best = 0;
+        st.ret_current = 0;
+        st.done = c.dead || (c.mode != FMPNP_MODE_COMPUTE_COST && c.n_iters <= 0);
+        st.abort_flag = 0;
+    }
+    __syncthreads();
+    // this workgroup's points -> LDS once per problem
+    const Ctx &c = st.c;
+    double *X = lds_X(mmax);
+    const double *src = c.pts + 3 * (size_t)c.p0;
+    for (int e = tid; e < 3 * c.M; e += NT) X[e] = src[e];
+    int *tex = lds_tex(mmax);
+    for (int i = tid; i < mmax; i += NT) tex[i] = -2;  // no texel cached yet
+    __syncthreads();
+}
+
+__device__ __forceinline__ void problem_end() {
+    LMState &st = S();
+    if (threadIdx.x == 0) {
+        if (st.abort_flag) {
+            st.c.dead = 1;
+            st.status |= FMPNP_STATUS_SYNC_TIMEOUT;
+        }
+        if (st.c.s == 0) {
+            fmpnp_result &r = st.c.results[st.c.p];
+            const bool cur = st.ret_current || st.c.mode == FMPNP_MODE_COMPUTE_COST;
+            for (int k = 0; k < 9; ++k) r.R[k] = cur ? st.R[k] : st.Rb[k];
+            for (int k = 0; k < 3; ++k) r.t[k] = cur ? st.t[k] : st.tb[k];
+            r.initial_cost = st.initial;
+            r.best_cost = st.has_best ? st.best : NAN;
+            r.final_lambda = st.lambda;
+            r.final_lr = st.lr;
+            r.best_num_inliers = st.has_best ? st.best_inl : -1;
+            r.n_evals = st.n_evals;
+            r.n_steps = st.n_steps;
+            r.n_accepted = st.n_accepted;
+            r.status = st.status;
+            r.has_best = st.has_best;
+        }
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// A: channel sums, one half-wave (32 lanes) per point, two points per wave.  Lane l of
+// a half owns channels cb + l*V + r*32*V + k (k < V, V = 16 B / sizeof(T)) and
+// accumulates them in (r, k) order in BOTH forms, so the vector form (16-byte loads)
+// and the scalar form (unaligned / ragged channel ranges) give bit-identical sums.  At
+// C = 256 fp32 a point is two rounds whose 8 loads per lane are all issued before the
+// first use: f, gx, gy and fref of a point arrive in ONE memory round trip.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void acc6(double a[8], double f, double r, double gx, double gy) {
+    double e = f - r;
+    a[0] = fma(e, e, a[0]);
+    a[1] = fma(gx, e, a[1]);
+    a[2] = fma(gy, e, a[2]);
+    a[3] = fma(gx, gx, a[3]);
+    a[4] = fma(gx, gy, a[4]);
+    a[5] = fma(gy, gy, a[5]);
+}
+
+template <typename VT>
+__device__ __forceinline__ VT gload(const void *p) {  // global (not flat) 16-byte load
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *reinterpret_cast<const __attribute__((address_space(1))) VT *>(reinterpret_cast<uintptr_t>(p));
+#else
+    return *reinterpret_cast<const VT *>(p);  // host pass: never executed
+#endif
+}
+
+template <typename T, bool VEC>
+__device__ __forceinline__ void gather_half(const T *__restrict__ t, const T *__restrict__ rf, int cs, int cb,
+                                            int ce, int l32, double a[8]) {
+    using VT = typename V16<T>::type;
+    constexpr int V = V16<T>::n;
+    if constexpr (VEC) {
+        // two rounds per trip, all eight loads issued before the first use (one round trip
+        // for C <= 64 V); a missing second round reads round one again and adds exact zeros
+        for (int c = cb + l32 * V; c < ce; c += 64 * V) {
+            const bool has2 = c + 32 * V < ce;
+            const int c2 = has2 ? c + 32 * V : c;
+            const VT f0 = gload<VT>(t + c), x0 = gload<VT>(t + cs + c), y0 = gload<VT>(t + 2 * cs + c);
+            const VT q0 = gload<VT>(rf + c);
+            const VT f1 = gload<VT>(t + c2), x1 = gload<VT>(t + cs + c2), y1 = gload<VT>(t + 2 * cs + c2);
+            const VT q1 = gload<VT>(rf + c2);
+            const T *pf = reinterpret_cast<const T *>(&f0), *px = reinterpret_cast<const T *>(&x0);
+            const T *py = reinterpret_cast<const T *>(&y0), *pr = reinterpret_cast<const T *>(&q0);
+#pragma unroll
+            for (int k = 0; k < V; ++k) acc6(a, (double)pf[k], (double)pr[k], (double)px[k], (double)py[k]);
+            const T *sf = reinterpret_cast<const T *>(&f1), *sx = reinterpret_cast<const T *>(&x1);
+            const T *sy = reinterpret_cast<const T *>(&y1), *sr = reinterpret_cast<const T *>(&q1);
+#pragma unroll
+            for (int k = 0; k < V; ++k) {
+                const double z = 0.0;
+                acc6(a, has2 ? (double)sf[k] : z, has2 ? (double)sr[k] : z, has2 ? (double)sx[k] : z,
+                     has2 ? (double)sy[k] : z);
+            }
+        }
+    } else {
+        for (int c = cb + l32 * V; c < ce; c += 32 * V) {
+#pragma unroll
+            for (int k = 0; k < V; ++k)
+                if (c + k < ce)
+                    acc6(a, (double)t[c + k], (double)rf[c + k], (double)t[cs + c + k], (double)t[2 * cs + c + k]);
+        }
+    }
+}
+
+// Transposed reduction of 8 values over the 32 lanes of a half-wave: halving exchanges
+// at bit 4 (permlane16 swap), bit 3 (row mirror), bit 2 (half-row mirror), then
+// butterflies at bits 1, 0 -- no LDS traffic.  Returns the half's total of value index
+// 4*b4 + 2*b3 + b2 of the lane; only equal indices are ever added.
+__device__ __forceinline__ double reduce8_in32(double v[8], int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        double a = v[i], b = v[i + 4];
+        swap16(a, b);  // even rows keep index i, odd rows i + 4
+        v[i] = a + b;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) v[i] = tstep<DPP_MIRROR16>(v[i], v[i + 2], lane & 8);
+    v[0] = tstep<DPP_MIRROR8>(v[0], v[1], lane & 4);
+    v[0] = v[0] + dpp64<DPP_XOR2>(v[0]);
+    return v[0] + dpp64<DPP_XOR1>(v[0]);
+}
+
+// Transposed reduction of 8 values over the 16 lanes of a row (DPP only): halving at
+// bits 3, 2, 1 then a butterfly at bit 0.  Returns the row total of value index
+// 4*b3 + 2*b2 + b1 of l16.
+__device__ __forceinline__ double reduce8_in16(double v[8], int l16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = tstep<DPP_MIRROR16>(v[i], v[i + 4], l16 & 8);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) v[i] = tstep<DPP_MIRROR8>(v[i], v[i + 2], l16 & 4);
+    v[0] = tstep<DPP_XOR2>(v[0], v[1], l16 & 2);
+    return v[0] + dpp64<DPP_XOR1>(v[0]);
+}
+
+// Transposed reduction of the 32-value vector over all 64 lanes of a wave.  `val(k)`
+// yields value k of the lane; values are produced in pairs (i, i+16) and folded at once by
+// the permlane32 swap (bit 5), so at most 16 doubles are live; then bit 4 (permlane16 swap)
+// and the in-row DPP steps.  Lane l returns the wave total of value index
+// 16*b5 + 8*b4 + 4*b3 + 2*b2 + b1 (b0 duplicates).  Only equal indices are ever added.
+template <typename F>
+__device__ __forceinline__ double reduce32_in64(F &&val, int lane) {
+    double v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        double a = val(i), b = val(i + 16);
+        swap32(a, b);  // low half keeps index i, high half i + 16
+        v[i] = a + b;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        double a = v[i], b = v[i + 8];
+        swap16(a, b);  // even rows keep index i, odd rows i + 8
+        v[i] = a + b;
+    }
+    return reduce8_in16(v, lane & 15);
+}
+__device__ __forceinline__ int reduce32_index(int lane) {
+    return 16 * ((lane >> 5) & 1) + 8 * ((lane >> 4) & 1) + 4 * ((lane >> 3) & 1) + 2 * ((lane >> 2) & 1) +
+           ((lane >> 1) & 1);
+}
+
+// ---------------------------------------------------------------------------
+// Ratio test (model.py:120-129): the team's max |rho| (order-free: exact) from every
+// wave's maximum.  Returns false on abort.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool ratio_exchange(double lmax) {
+    LMState &st = S();
+    const Ctx &c = st.c;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    lmax = wave_nanmax(lmax);
+    if (lane == 0) st.wg_max[wave] = lmax;
+    __syncthreads();
+    if (tid == 0) {
+        double m = st.wg_max[0];
+        for (int w = 1; w < NT / 64; ++w) m = nanmax(m, st.wg_max[w]);
+        st.rho_max = m;
+        if (c.G > 1) st_sc1(c.max_g + ((c.epoch + 1) & 1) * c.G + c.s, m);
+    }
+    if (c.G > 1) {
+        team_arrive();
+        if (tid < 64 && team_wait() && tid == 0) {
+            double m = -1.0;
+            for (int w = 0; w < c.G; ++w) m = nanmax(m, ld_sc1(c.max_g + (c.epoch & 1) * c.G + w));
+            st.rho_max = m;
+        }
+    }
+    __syncthreads();
+    return !st.abort_flag;
+}
+
+// ---------------------------------------------------------------------------
+// B2: per-point normal-equation contributions -> one 32-double partial per chunk
+// (LDS when G == 1, the team's global slot with sc1 stores when G > 1).
+// ---------------------------------------------------------------------------
+// value index -> (row, col) of the upper triangle of H (0..20), then g (21..26)
+__device__ __forceinline__ constexpr int h_row(int k) {
+    return k < 6 ? 0 : k < 11 ? 1 : k < 15 ? 2 : k < 18 ? 3 : k < 20 ? 4 : 5;
+}
+__device__ __forceinline__ constexpr int h_col(int k) {
+    return k < 6 ? k : k < 11 ? k - 5 : k < 15 ? k - 9 : k < 18 ? k - 12 : k < 20 ? k - 14 : 5;
+}
+
+// One 64-point block of a wave: lane = point.  Points that do not contribute get w = 0
+// and a harmless geometry (z = 1).  Writes the block's partial (one chunk: LDS when
+// G == 1, the team's global slot `dst_g` with sc1 stores when G > 1).
+__device__ __forceinline__ void contrib_block(const PC &q, int mmax, int blk, bool sup, bool kept, double rho,
+                                              double d1, const double *r, const double Pc[3], double *dst_g) {
+    const int lane = threadIdx.x & 63;
+    const double fx = q.K[0], fy = q.K[4];
+    const int lc = blk;  // one chunk per 64-point block
+    const double w = kept ? d1 : 0.0, rh = kept ? rho : 0.0;
+    const double P0 = kept ? Pc[0] : 0.0, P1 = kept ? Pc[1] : 0.0, z = kept ? Pc[2] : 1.0;
+    const double sex = kept ? r[1] : 0.0, sey = kept ? r[2] : 0.0;
+    const double sxx = kept ? r[3] : 0.0, sxy = kept ? r[4] : 0.0, syy = kept ? r[5] : 0.0;
+    // J_px_p (model.py:377-382) times J_p_T (model.py:369-370): A (2x6), A0[1] = A1[0] = 0
+    // one reciprocal instead of six divisions (Jacobian entries only: last-bit level)
+    const double iz = recip(z);
+    const double j00 = fx * iz, j02 = ((-fx) * P0 * iz) * iz;
+    const double j11 = fy * iz, j12 = ((-fy) * P1 * iz) * iz;
+    const double A0[6] = {j00, 0.0, j02, j02 * P1, j00 * z - j02 * P0, -j00 * P1};
+    const double A1[6] = {0.0, j11, j12, -j11 * z + j12 * P1, -j12 * P0, j11 * P0};
+    // w folded into the 2x2 channel moments; the structural zeros A0[1] = A1[0] = 0 are
+    // skipped explicitly (IEEE arithmetic cannot drop 0 * x by itself)
+    const double wxx = w * sxx, wxy = w * sxy, wyy = w * syy, wex = w * sex, wey = w * sey;
+    double M0[6], M1[6];  // (w S) A: M0 = row x, M1 = row y
+    M0[0] = wxx * A0[0];
+    M1[0] = wxy * A0[0];
+    M0[1] = wxy * A1[1];
+    M1[1] = wyy * A1[1];
+#pragma unroll
+    for (int l = 2; l < 6; ++l) {
+        M0[l] = wxx * A0[l] + wxy * A1[l];
+        M1[l] = wxy * A0[l] + wyy * A1[l];
+    }
+    auto val = [&](int k) -> double {
+        if (k < 21) {  // H[a][b] = A_a^T (w S) A_b
+            const int a = h_row(k), b = h_col(k);
+            return a == 0 ? A0[0] * M0[b] : a == 1 ? A1[1] * M1[b] : A0[a] * M0[b] + A1[a] * M1[b];
+        } else if (k < 27) {  // g = A^T (w G^T e)
+            const int l = k - 21;
+            return l == 0 ? A0[0] * wex : l == 1 ? A1[1] * wey : A0[l] * wex + A1[l] * wey;
+        } else if (k == 27) {
+            return rh;
+        } else if (k == 28) {
+            return kept ? 1.0 : 0.0;
+        } else if (k == 29) {
+            return sup ? 1.0 : 0.0;
+        }
+        return 0.0;
+    };
+    const double tot = reduce32_in64(val, lane);
+    if (lc < q.LC && (lane & 1) == 0) {
+        const int idx = reduce32_index(lane);
+        if (q.G == 1) lds_part(mmax)[(size_t)(q.c0 + lc) * NV + idx] = tot;  // G == 1 (LDS)
+        else st_sc1(dst_g + (size_t)(q.c0 + lc) * NV + idx, tot);
+    }
+}
+
+// The eight 16-byte loads of one point's texel for one half-wave lane (C <= 64 V channels:
+// a point is one memory round trip), issued ahead of their use so that the next pair's
+// loads are in flight while the current pair is reduced.
+template <typename T>
+struct GLoad {
+    typename V16<T>::type f0, x0, y0, q0, f1, x1, y1, q1;
+};
+template <typename T>
+__device__ __forceinline__ void g_issue(GLoad<T> &g, const T *t, const T *rf, int cs, int c, int c2) {
+    using VT = typename V16<T>::type;
+    g.f0 = gload<VT>(t + c);
+    g.x0 = gload<VT>(t + cs + c);
+    g.y0 = gload<VT>(t + 2 * cs + c);
+    g.q0 = gload<VT>(rf + c);
+    g.f1 = gload<VT>(t + c2);
+    g.x1 = gload<VT>(t + cs + c2);
+    g.y1 = gload<VT>(t + 2 * cs + c2);
+    g.q1 = gload<VT>(rf + c2);
+}
+// Same accumulation order as gather_half<T, true> (round one, then round two or exact
+// zeros), so both paths give bit-identical sums; has1 = false lanes add nothing.
+// FULL: every lane has both rounds (C == 64 V, e.g. C = 256 fp32): no per-lane selects.
+template <typename T, bool FULL>
+__device__ __forceinline__ void g_consume(const GLoad<T> &g, bool has1, bool has2, double a[8]) {
+    constexpr int V = V16<T>::n;
+    if (FULL) has1 = has2 = true;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = 0.0;
+    if (!has1) return;
+    const T *pf = reinterpret_cast<const T *>(&g.f0), *px = reinterpret_cast<const T *>(&g.x0);
+    const T *py = reinterpret_cast<const T *>(&g.y0), *pr = reinterpret_cast<const T *>(&g.q0);
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc6(a, (double)pf[k], (double)pr[k], (double)px[k], (double)py[k]);
+    const T *sf = reinterpret_cast<const T *>(&g.f1), *sx = reinterpret_cast<const T *>(&g.x1);
+    const T *sy = reinterpret_cast<const T *>(&g.y1), *sr = reinterpret_cast<const T *>(&g.q1);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        const double z = 0.0;
+        acc6(a, has2 ? (double)sf[k] : z, has2 ? (double)sr[k] : z, has2 ? (double)sx[k] : z,
+             has2 ? (double)sy[k] : z);
+    }
+}
+
+// Pair selection from a dirty mask: the half-waves take the two lowest set lanes.
+struct GPair {
+    int j;      // this half-wave's point (lane index in the block)
+    int to;     // its texel offset
+    bool two;   // a second point exists (the high half's point is real)
+};
+__device__ __forceinline__ GPair pick_pair(unsigned long long &m, int off, bool hi) {
+    const int a = __builtin_ctzll(m);
+    m &= m - 1;
+    const bool two = m != 0;
+    const int b = two ? __builtin_ctzll(m) : a;
+    if (two) m &= m - 1;
+    const int oa = __builtin_amdgcn_readlane(off, a), ob = __builtin_amdgcn_readlane(off, b);
+    return GPair{hi ? b : a, hi ? ob : oa, two};
+}
+
+// Bilinear channel sums of one point for one half-wave lane (FMPNP_BILINEAR): the four
+// taps' f, gx, gy and fref of the lane's channels per round (13 loads of 16 B at fp32),
+// sampled with the point's weights (sample4) and accumulated like the nearest gather.
+template <typename T, bool VEC>
+__device__ __forceinline__ void gather_bil_half(const T *__restrict__ feat, const int o[4], const double w[4],
+                                                const T *__restrict__ rf, int cs, int cb, int ce, int l32,
+                                                double a[8]) {
+    using VT = typename V16<T>::type;
+    constexpr int V = V16<T>::n;
+    const T *t0 = feat + (size_t)o[0] * 3 * cs, *t1 = feat + (size_t)o[1] * 3 * cs;
+    const T *t2 = feat + (size_t)o[2] * 3 * cs, *t3 = feat + (size_t)o[3] * 3 * cs;
+    if constexpr (VEC) {
+        for (int c = cb + l32 * V; c < ce; c += 32 * V) {
+            VT f[4], x[4], y[4];
+            const T *tp[4] = {t0, t1, t2, t3};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                f[k] = gload<VT>(tp[k] + c);
+                x[k] = gload<VT>(tp[k] + cs + c);
+                y[k] = gload<VT>(tp[k] + 2 * cs + c);
+            }
+            const VT q = gload<VT>(rf + c);
+            const T *pq = reinterpret_cast<const T *>(&q);
+            const T *pf[4], *px[4], *py[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                pf[k] = reinterpret_cast<const T *>(&f[k]);
+                px[k] = reinterpret_cast<const T *>(&x[k]);
+                py[k] = reinterpret_cast<const T *>(&y[k]);
+            }
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+                acc6(a, sample4(w, pf[0][e], pf[1][e], pf[2][e], pf[3][e]), (double)pq[e],
+                     sample4(w, px[0][e], px[1][e], px[2][e], px[3][e]),
+                     sample4(w, py[0][e], py[1][e], py[2][e], py[3][e]));
+        }
+    } else {
+        for (int c = cb + l32 * V; c < ce; c += 32 * V) {
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+                if (c + e < ce) {
+                    const int ch = c + e;
+                    acc6(a, sample4(w, t0[ch], t1[ch], t2[ch], t3[ch]), (double)rf[ch],
+                         sample4(w, t0[cs + ch], t1[cs + ch], t2[cs + ch], t3[cs + ch]),
+                         sample4(w, t0[2 * cs + ch], t1[2 * cs + ch], t2[2 * cs + ch], t3[2 * cs + ch]));
+                }
+        }
+    }
+}
+
+// Every supported point of a block, two per trip (one per half-wave); each half-wave takes
+// its point's taps from the point's lane.
+template <typename T>
+__device__ __forceinline__ void gather_bil_block(unsigned long long m, const Taps &tp, bool hi, int lane,
+                                                 const T *feat, const T *fref0, int cs, int cb, int ce, int ld,
+                                                 bool vec, double *rec0, int e6, bool wlane) {
+    const int l32 = lane & 31;
+    while (m) {
+        const int pa = __builtin_ctzll(m);
+        m &= m - 1;
+        const bool two = m != 0;
+        const int pb = two ? __builtin_ctzll(m) : pa;
+        if (two) m &= m - 1;
+        const int src = hi ? pb : pa;
+        int o[4];
+        double w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int oa = __builtin_amdgcn_readlane(tp.off[k], pa), ob = __builtin_amdgcn_readlane(tp.off[k], pb);
+            const double wa = rlane64(tp.w[k], pa), wb = rlane64(tp.w[k], pb);
+            o[k] = hi ? ob : oa;
+            w[k] = hi ? wb : wa;
+        }
+        double v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = 0.0;
+        const T *rf = fref0 + (size_t)src * ld;
+        if (vec) gather_bil_half<T, true>(feat, o, w, rf, cs, cb, ce, l32, v);
+        else gather_bil_half<T, false>(feat, o, w, rf, cs, cb, ce, l32, v);
+        const double r = reduce8_in32(v, lane);
+        if (wlane && (!hi || two)) rec0[(size_t)src * RECW + e6] = r;
+    }
+}
+
+// Double-buffered pair gathers of one block: the next pair's loads are issued before this
+// pair's channel sums are reduced (one exposed round trip per block, not one per pair).
+// fref0 / rec0: the block's first descriptor row and record.
+template <typename T, bool FULL>
+__device__ __forceinline__ void gather_pipe(unsigned long long m, int off, bool hi, int lane, const T *feat,
+                                            const T *fref0, int cs, int ld, int gc1, int gc2, bool has1, bool has2,
+                                            double *rec0, int e6, bool wlane) {
+    if (!m) return;
+    GLoad<T> A, B;
+    GPair pa = pick_pair(m, off, hi), pb;
+    g_issue<T>(A, feat + (size_t)pa.to * 3 * cs, fref0 + (size_t)pa.j * ld, cs, gc1, gc2);
+    while (true) {
+        const bool moreB = m != 0;
+        if (moreB) {
+            pb = pick_pair(m, off, hi);
+            g_issue<T>(B, feat + (size_t)pb.to * 3 * cs, fref0 + (size_t)pb.j * ld, cs, gc1, gc2);
+        }
+        {
+            double v[8];
+            g_consume<T, FULL>(A, has1, has2, v);
+            const double r = reduce8_in32(v, lane);
+            if (wlane && (!hi || pa.two)) rec0[(size_t)pa.j * RECW + e6] = r;
+        }
+        if (!moreB) break;
+        const bool moreA = m != 0;
+        if (moreA) {
+            pa = pick_pair(m, off, hi);
+            g_issue<T>(A, feat + (size_t)pa.to * 3 * cs, fref0 + (size_t)pa.j * ld, cs, gc1, gc2);
+        }
+        {
+            double v[8];
+            g_consume<T, FULL>(B, has1, has2, v);
+            const double r = reduce8_in32(v, lane);
+            if (wlane && (!hi || pb.two)) rec0[(size_t)pb.j * RECW + e6] = r;
+        }
+        if (!moreA) break;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// One evaluation at (Re, te) over the wave's blocks (no workgroup barrier inside).
+// Without the ratio test each block goes straight on to its chunk partials; with it the
+// loss values are parked in the records and the wave's max |rho| is returned.
+// PIPE: double-buffered gathers (latency variant: the VGPRs for two pairs in flight).
+// ---------------------------------------------------------------------------
+template <typename T, bool PIPE>
+__device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ngath) {
+    LMState &st = S();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l32 = lane & 31;
+    const bool hi = lane >= 32;
+    const double *X = lds_X(mmax);
+    double *rec = lds_rec(mmax);
+    int *tex = lds_tex(mmax);
+    const T *feat = reinterpret_cast<const T *>(q.feat);
+    const T *fref = reinterpret_cast<const T *>(q.fref);
+    const int cs = q.cs, cb = q.cb, ce = q.ce, p0 = q.p0, ld = q.ld, M = q.M;
+    constexpr int V = V16<T>::n;
+    const bool vec = ((((uintptr_t)feat) | ((uintptr_t)fref)) & 15) == 0 && cs % V == 0 && ld % V == 0 &&
+                     cb % V == 0 && (ce - cb) % V == 0;
+    // one round trip per point: every channel of the slice within the two rounds of a lane
+    const bool onetrip = vec && ce - cb <= 64 * V;
+    const int gc = cb + l32 * V;                    // this lane's first channel (one-trip path)
+    const bool has1 = gc < ce, has2 = gc + 32 * V < ce;
+    const int gc1 = has1 ? gc : cb, gc2 = has2 ? gc + 32 * V : gc1;
+    const bool defer = q.use_ratio != 0;
+    double *dst_g = q.part_g;
+    if (q.G > 1) dst_g += (size_t)((ufirst((int)st.c.epoch) + 1) & 1) * q.nc_max * NV;
+    // the pose evaluated: one LDS broadcast read per evaluation, kept in VGPRs (moving it to
+    // SGPRs costs 24 v_readfirstlane and SGPR spills)
+    double Re[9], te[3];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Re[k] = st.Re[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) te[k] = st.te[k];
+    double lmax = -1.0;  // -1: nothing supported seen yet
+    for (int blk = wave; blk * 64 < M; blk += NT / 64) {
+        const int i = blk * 64 + lane;
+        const bool valid = i < M;
+        // projection (model.py:303-311) and indexing_ (model.py:88-89): floor(y*Hf/H),
+        // floor(x*Wf/W) of the reference's fp64 expression equal the integer quotients
+        // (exact products, a correctly rounded quotient of integers floors to the integer
+        // quotient), computed here with invariant-multiplier division
+        double Pc[3] = {0.0, 0.0, 1.0};
+        int off = -1;
+        Taps tp;
+        if (valid) {
+            transform_pt(Re, te, X[3 * i], X[3 * i + 1], X[3 * i + 2], Pc);
+            int x, y;
+            double qx, qy;
+            if (project_px(q.K, Pc, q.im_w, q.im_h, x, y, qx, qy)) {
+                const int row = (int)udiv((unsigned)y * (unsigned)q.Hf, q.dh);
+                const int col = (int)udiv((unsigned)x * (unsigned)q.Wf, q.dw);
+                off = row * q.Wf + col;
+                if (q.bilinear) bilinear_taps(qx, qy, q.Hf, q.Wf, q.im_w, q.im_h, tp);
+            }
+        }
+        // memoised gather: a point whose texel did not change keeps its record (the six
+        // channel sums depend only on the texel and the point's fixed descriptor)
+        const int old = valid ? tex[i] : -1;
+        // (bilinear: the taps' weights move with the pose, every supported point is sampled)
+        const bool dirty = off >= 0 && (off != old || q.no_memo || q.bilinear);
+        if (valid) tex[i] = off;
+        unsigned long long m = __ballot(dirty);
+        ngath += __popcll(m);
+        dbg_stamp(q.stamps, 0);
+        const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
+        const bool wlane = (lane & 3) == 0 && e6 < 6;
+        if (q.bilinear) {
+            gather_bil_block<T>(m, tp, hi, lane, feat, fref + (size_t)(p0 + blk * 64) * ld, cs, cb, ce, ld, vec,
+                                rec + (size_t)blk * 64 * RECW, e6, wlane);
+        } else if (PIPE && onetrip) {
+            // double-buffered pairs: the next pair's loads are issued before this pair's
+            // channel sums are reduced (one exposed round trip per block, not one per pair)
+            if (ce - cb == 64 * V)
+                gather_pipe<T, true>(m, off, hi, lane, feat + 0, fref + (size_t)(p0 + blk * 64) * ld, cs, ld, gc1, gc2,
+                                     has1, has2, rec + (size_t)blk * 64 * RECW, e6, wlane);
+            else
+                gather_pipe<T, false>(m, off, hi, lane, feat + 0, fref + (size_t)(p0 + blk * 64) * ld, cs, ld, gc1,
+                                      gc2, has1, has2, rec + (size_t)blk * 64 * RECW, e6, wlane);
+        } else {
+            while (m) {  // wave-uniform: two dirty points per trip, one per half-wave
+                const GPair pp = pick_pair(m, off, hi);
+                const int ii = blk * 64 + pp.j;
+                const T *t = feat + (size_t)pp.to * 3 * cs;
+                const T *rf = fref + (size_t)(p0 + ii) * ld;
+                double v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = 0.0;
+                if (vec) gather_half<T, true>(t, rf, cs, cb, ce, l32, v);
+                else gather_half<T, false>(t, rf, cs, cb, ce, l32, v);
+                const double r = reduce8_in32(v, lane);
+                if (wlane && (!hi || pp.two)) rec[(size_t)ii * RECW + e6] = r;
+            }
+        }
+        // the records just written are read by other lanes of this wave: LDS operations of
+        // a wave complete in order; the clobber keeps the compiler from reordering them
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        dbg_stamp(q.stamps, 1);
+        const bool sup = off >= 0;
+        const double *r = rec + (size_t)(valid ? i : 0) * RECW;
+        double rho = 0.0, d1 = 0.0;
+        if (sup) loss_eval(q.loss, q.alpha, 0.5 * r[0], rho, d1);
+        if (defer) {
+            if (valid) {
+                rec[(size_t)i * RECW + 6] = rho;
+                rec[(size_t)i * RECW + 7] = d1;
+            }
+            if (sup) lmax = nanmax(lmax, fabs(rho));
+        } else {
+            contrib_block(q, mmax, blk, sup, sup, rho, d1, r, Pc, dst_g);
+        }
+        dbg_stamp(q.stamps, 2);
+    }
+    return lmax;
+}
+
+// Second pass of the ratio test: the weights of points with |rho| >= max|rho| * thr
+// are zero (model.py:324-336); P is recomputed bit-identically from X.
+__device__ __forceinline__ void contrib_pass(const PC &q, int mmax) {
+    LMState &st = S();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const double *X = lds_X(mmax);
+    const double *rec = lds_rec(mmax);
+    const int *tex = lds_tex(mmax);
+    const double limit = ufirst(st.rho_max) * st.c.ratio_thr;
+    double *dst_g = q.part_g;
+    if (q.G > 1) dst_g += (size_t)((ufirst((int)st.c.epoch) + 1) & 1) * q.nc_max * NV;
+    double Re[9], te[3];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Re[k] = ufirst(st.Re[k]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) te[k] = ufirst(st.te[k]);
+    for (int blk = wave; blk * 64 < q.M; blk += NT / 64) {
+        const int i = blk * 64 + lane;
+        const bool valid = i < q.M;
+        const bool sup = valid && tex[i] >= 0;
+        double Pc[3] = {0.0, 0.0, 1.0};
+        if (sup) transform_pt(Re, te, X[3 * i], X[3 * i + 1], X[3 * i + 2], Pc);
+        const double *r = rec + (size_t)(valid ? i : 0) * RECW;
+        const bool kept = sup && fabs(r[6]) < limit;
+        contrib_block(q, mmax, blk, sup, kept, r[6], r[7], r, Pc, dst_g);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Combine on wave 0 (after the barrier / team exchange): the ordered sum over chunk
+// (= block) indices.  Lane (j, h) (value j = lane & 31, half h = lane >> 5) sums chunks
+// h, h+2, h+4, ... in order; the halves are then added.  Depends only on the chunk
+// partials and NC -- not on G, placement or timing.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double combine_final_wave(int mmax, bool team) {
+    LMState &st = S();
+    const Ctx &c = st.c;
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    const int NC = c.NC;
+    double t = 0.0;
+    if (!team) {
+        const double *src = lds_part(mmax);
+        double v[4];
+        for (int r0 = h; r0 < NC; r0 += 8) {  // four loads in flight, adds in chunk order
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = r0 + 2 * u < NC ? src[(r0 + 2 * u) * NV + j] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (r0 + 2 * u < NC) t += v[u];
+        }
+    } else {
+        const double *src = c.part_g + (size_t)(c.epoch & 1) * c.nc_max * NV;
+        double v[4];
+        for (int r0 = h; r0 < NC; r0 += 8) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = r0 + 2 * u < NC ? ld_sc1(src + (r0 + 2 * u) * NV + j) : 0.0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (r0 + 2 * u < NC) t += v[u];
+        }
+    }
+    double a = t, b = t;
+    swap32(a, b);  // low half: (own, partner); high half: (partner, own)
+    const double tot = a + b;  // even chunks + odd chunks, in both halves
+    if (lane < NV) st.tot[lane] = tot;  // for the solve's broadcast reads
+    return tot;
+}
+
+// ---------------------------------------------------------------------------
+// 6x6 damped solve on one wave: lanes 0..5 own the rows of H + lambda diag(diag(H)+1e-9)
+// (model.py:46-48) and run LU with partial pivoting (model.py:51,61) row-parallel.
+// Pivot choice = the serial scan's (first position with the largest |A[.][j]|), the
+// elimination and the forward substitution are the serial arithmetic; the back
+// substitution runs column-wise with the pivots' reciprocals.  Uniform values move
+// between lanes with v_readlane only.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double rlane(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__host__ __device__ constexpr int tri6(int i, int j) { return i * 6 - (i * (i - 1)) / 2 + (j - i); }
+
+__device__ __forceinline__ void lm_step_rows(const double *Hu, const double *g, double lambda, double lr,
+                                             double delta[6]) {
+    const int lane = threadIdx.x & 63;
+    const int r = lane < 6 ? lane : 5;
+    double A[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) A[c] = Hu[r <= c ? tri6(r, c) : tri6(c, r)];
+    double b = g[r];
+    if (lambda != 0.0) {
+#pragma unroll
+        for (int c = 0; c < 6; ++c)
+            if (c == r) A[c] = A[c] + (A[c] + 1e-9) * lambda;
+    }
+    int pos = lane < 6 ? lane : 64;  // current position of this lane's row (64: no row)
+    int lane_at[6] = {0, 1, 2, 3, 4, 5};
+    double inv[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const double rj = 1.0 / A[j];  // every row's candidate pivot reciprocal, off the critical path
+        int p = j;
+        double best = fabs(rlane(A[j], lane_at[j]));
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) {
+            const double v = fabs(rlane(A[j], lane_at[i]));
+            if (v > best) { best = v; p = i; }
+        }
+        const int lj = lane_at[j];
+        int lp = lj;
+#pragma unroll
+        for (int k = j + 1; k < 6; ++k) lp = (p == k) ? lane_at[k] : lp;
+#pragma unroll
+        for (int k = j + 1; k < 6; ++k) lane_at[k] = (p == k) ? lj : lane_at[k];
+        lane_at[j] = lp;
+        if (lane == lp) pos = j;
+        else if (lane == lj) pos = p;
+        double prow[6];
+#pragma unroll
+        for (int c = j + 1; c < 6; ++c) prow[c] = rlane(A[c], lp);
+        const double pb = rlane(b, lp);
+        const double iv = rlane(rj, lp);  // = 1 / A[p][j], computed before the pivot was known
+        inv[j] = iv;
+        if (pos > j && pos < 6) {
+            const double m = A[j] * iv;
+            A[j] = m;
+#pragma unroll
+            for (int c = j + 1; c < 6; ++c) A[c] -= m * prow[c];
+            b -= m * pb;
+        }
+    }
+    double x[6];
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {
+        const double xi = rlane(b, lane_at[i]) * inv[i];
+        x[i] = xi;
+        if (pos < i) b -= A[i] * xi;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) delta[i] = -lr * x[i];
+}
+
+// ---------------------------------------------------------------------------
+// Fast path of the damped solve: H + lambda diag(diag(H) + 1e-9) is symmetric positive
+// definite whenever lambda > 0 (H = sum rho' J^T J with rho' > 0 for every loss), so an
+// LDL^T factorisation needs no pivoting and no cross-lane traffic: every lane of wave 0
+// runs the same ~160 register-resident fp64 instructions.  The reference's LU solve
+// (model.py:51,61) and this one agree to rounding (cond(H) * eps, far inside the pose
+// tolerance; tests/test_gpu_parity.py).  Returns false -- and the caller falls back to
+// the pivoted LU -- when a pivot is not positive (lambda = 0 on a singular H, NaN).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool ldlt_step(const double *Hu, const double *g, double lambda, double lr,
+                                          double delta[6]) {
+    double a[6][6];  // lower triangle used: a[i][j], i >= j
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) a[i][j] = Hu[tri6(j, i)];
+    if (lambda != 0.0) {
+#pragma unroll
+        for (int j = 0; j < 6; ++j) a[j][j] = a[j][j] + (a[j][j] + 1e-9) * lambda;
+    }
+    double b[6], inv[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) b[i] = g[i];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        ok &= a[j][j] > 0.0;  // false for NaN
+        // reciprocal by v_rcp_f64 + one Newton step (~1 ulp; the solve is not bit-pinned to
+        // the reference's LU anyway) instead of a full IEEE division on the critical path
+        const double r0 = __builtin_amdgcn_rcp(a[j][j]);
+        inv[j] = fma(fma(-a[j][j], r0, 1.0), r0, r0);
+        double u[6];
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) u[i] = a[i][j];
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) {
+            const double l = u[i] * inv[j];
+#pragma unroll
+            for (int c = j + 1; c <= i; ++c) a[i][c] = fma(-l, u[c], a[i][c]);
+            b[i] = fma(-l, b[j], b[i]);  // forward substitution L y = g, folded in
+            a[i][j] = l;
+        }
+    }
+    double x[6];
+#pragma unroll
+    for (int j = 5; j >= 0; --j) {
+        double v = b[j] * inv[j];
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) v = fma(-a[i][j], x[i], v);
+        x[j] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) delta[i] = -lr * x[i];
+    return ok;
+}
+
+// ---------------------------------------------------------------------------
+// LM state machine (model.py:300-486) on wave 0.  The evaluation's totals arrive
+// lane-distributed (lane j holds value j, from the combine, which also stored them to
+// st.tot); the three the schedule needs are taken by v_readlane.  The scalar state and
+// this lane's pose elements (lane k < 12: R[k] for k < 9, t[k - 9]) are read in one LDS
+// burst; the pose and linearisation copies are lane-wise stores nothing waits on; the
+// solve and the pose update read their uniform operands by LDS broadcast.  Every team
+// member computes the same from identical totals.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void lm_update_wave(double tot, bool stamps) {
+    LMState &st = S();
+    const Ctx &c = st.c;
+    const int lane = threadIdx.x & 63;
+    const bool w0 = lane == 0;
+    const int kk = lane < 12 ? lane : 0;
+    static_assert(offsetof(LMState, Re) == offsetof(LMState, R) + 12 * sizeof(double), "R/t/Re/te layout");
+    static_assert(offsetof(LMState, hc) == offsetof(LMState, tot) + NV * sizeof(double), "tot/hc layout");
+    // LDS burst: scalar state and this lane's evaluated pose element
+    const double lam_s = st.lambda, lr_s = st.lr, prev = st.prev, best_s = st.best;
+    const int n_evals = st.n_evals, n_steps = st.n_steps;
+    const double pe = st.R[12 + kk];  // [Re | te][k]
+    const int mode = c.mode, n_iters = c.n_iters;
+    const double kept_d = rlane(tot, 28);
+    const int nsup = (int)rlane(tot, 29);
+    const int kept = (int)kept_d;
+    const double cost = rlane(tot, 27) / kept_d;  // torch mean of an empty tensor = NaN
+    if (mode == FMPNP_MODE_COMPUTE_COST) {
+        if (w0) {
+            st.initial = nsup == 0 ? NAN : cost;
+            if (nsup == 0) st.status |= FMPNP_STATUS_NO_SUPPORT;
+            st.n_evals = 1;
+            st.done = 1;
+        }
+        return;
+    }
+    const bool first = n_evals == 0;
+    if (nsup == 0) {  // model.py:316-320 / :441-445: return the current pose
+        if (w0) {
+            st.status |= first ? FMPNP_STATUS_NO_SUPPORT : FMPNP_STATUS_NO_SUPPORT_TRIAL;
+            st.ret_current = 1;
+            st.done = 1;
+        }
+        return;
+    }
+    double lambda = lam_s, lr = lr_s;
+    bool accepted = true;
+    if (!first) {  // model.py:469-478
+        accepted = !(cost > prev);
+        const double lam = lambda * (cost > prev ? 10.0 : 0.1);
+        lambda = lam < 1e-6 ? 1e-6 : (lam > 1e4 ? 1e4 : lam);
+        if (!accepted) {
+            const double l2 = 0.1 * lr;
+            lr = l2 < 1e-3 ? 1e-3 : (l2 > 1.0 ? 1.0 : l2);
+        } else {
+            lr = 1.0;
+        }
+    }
+    // the evaluated pose becomes current and its normal equations the linearisation
+    const bool take = first || accepted;
+    const bool new_best = !first && accepted && cost < best_s;
+    if (lane < 12) {
+        if (new_best) st.Rb[lane] = pe;  // [Rb | tb] contiguous
+        if (take) st.R[lane] = pe;       // [R | t]
+    }
+    if (take && lane < NV) st.hc[lane] = tot;
+    if (w0) {
+        if (first) {  // model.py:347-359
+            st.prev = st.best = st.initial = cost;
+            st.best_inl = kept;
+            st.has_best = 1;
+        } else if (accepted) {  // model.py:477-486
+            st.n_accepted++;
+            if (new_best) {
+                st.best_inl = kept;
+                st.best = cost;
+            }
+            st.prev = cost;
+        }
+        st.lambda = lambda;
+        st.lr = lr;
+        st.n_evals = n_evals + 1;
+    }
+    if (c.trace && c.s == 0 && n_evals < c.trace_stride) {
+        fmpnp_trace_entry &e = c.trace[(size_t)c.p * c.trace_stride + n_evals];
+        if (lane < 9) e.R[lane] = pe;
+        else if (lane < 12) e.t[lane - 9] = pe;
+        if (w0) {
+            e.cost = cost;
+            e.lambda_after = lambda;
+            e.lr_after = lr;
+            e.n_supported = nsup;
+            e.n_kept = kept;
+            e.accepted = accepted ? 1 : 0;
+        }
+    }
+    if (n_steps >= n_iters) {
+        if (w0) st.done = 1;
+        return;
+    }
+    // next step from the linearisation at the current pose (model.py:408-426); uniform
+    // operands by LDS broadcast (this wave's own stores above: LDS is in order per wave)
+    const double *hs = st.tot + (take ? 0 : NV);
+    double Hu[21], gv[6], delta[6];
+#pragma unroll
+    for (int k = 0; k < 21; ++k) Hu[k] = hs[k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) gv[k] = hs[21 + k];
+    dbg_stamp(stamps, 5);  // LM bookkeeping
+    // (the pivoted-LU fallback indexes H by lane: it reads the LDS copy, not a private array)
+    if (!ldlt_step(Hu, gv, lambda, lr, delta)) lm_step_rows(hs, hs + 21, lambda, lr, delta);
+    dbg_stamp(stamps, 6);  // 6x6 solve
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) bad |= isnan(delta[k]);
+    if (bad) {  // model.py:411-413
+        if (w0) {
+            st.n_steps = n_steps + 1;
+            st.status |= FMPNP_STATUS_NAN;
+            st.done = 1;
+        }
+        return;
+    }
+    const double *pp = st.R + (take ? 12 : 0);  // [R | t] or [Re | te]
+    double Rc[9], tc[3], Rn[9], tn[3];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Rc[k] = pp[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) tc[k] = pp[9 + k];
+    pose_update(Rc, tc, delta, Rn, tn);
+    if (w0) {
+        st.n_steps = n_steps + 1;
+        for (int k = 0; k < 9; ++k) st.Re[k] = Rn[k];
+        for (int k = 0; k < 3; ++k) st.te[k] = tn[k];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// the kernel
+// ---------------------------------------------------------------------------
+// Specialised per launch (the launcher picks the variant): TEAM = G > 1, RATIO = the ratio
+// test is on, VAR = VAR_GM (Geman-McClure forward, nearest sampling: the common case),
+// VAR_NEAREST (any loss / mode, nearest) or VAR_BILINEAR -- constant-folding the other
+// paths out shortens the per-point code and frees registers.
+template <typename T, int WPS, bool TEAM, bool RATIO, int VAR>
+__global__ __launch_bounds__(NT, WPS) void lm_kernel(LaunchArgs a) {
+    LMState &st = S();
+    const int G = a.G;
+    // XCD-aware team placement: members of one team share blockIdx % gw (the same XCD
+    // under the observed round-robin dispatch; speed only, never correctness).
+    const int b = blockIdx.x, gw = a.gw;
+    const int grp = b / (gw * G), rem = b % (gw * G);
+    const int s = rem / gw;
+    const int team = grp * gw + rem % gw;
+    if (team >= a.teams) return;
+    const int tid = threadIdx.x;
+    const int mmax = a.mmax;
+    if (tid == 0) {
+        Ctx &c = st.c;
+        c.results = a.results;
+        c.trace = a.trace;
+        c.trace_stride = a.trace_stride;
+        c.counter = a.counters + team * 16;
+        c.part_g = a.partials + (size_t)team * 2 * a.nc_max * NV;
+        c.max_g = a.maxslots + (size_t)team * 2 * G;
+        c.nc_max = a.nc_max;
+        c.lambda0 = a.opt.lambda0;
+        c.ratio_thr = a.opt.ratio_threshold;
+        c.alpha = a.opt.barron_alpha;
+        c.mode = a.opt.mode;
+        c.n_iters = a.opt.n_iters;
+        c.use_ratio = a.opt.use_ratio;
+        c.loss = a.opt.loss;
+        c.no_memo = a.opt.no_memo;
+        c.sampling = a.opt.sampling;
+        c.stamps_on = a.stamps != nullptr;
+        c.G = G;
+        c.s = s;
+        c.epoch = 0;
+        c.dead = 0;
+    }
+    __syncthreads();
+    // optional phase stamps (debug: a.stamps != null): s_memtime deltas on thread 0
+    const bool stamps_on = a.stamps != nullptr;
+    if (stamps_on && (tid & 63) == 0) {
+        for (int k = 0; k < NSTAMP; ++k) st.stamp_ph[tid >> 6][k] = 0;
+        st.stamp_t[tid >> 6] = __builtin_amdgcn_s_memtime();
+    }
+    for (int p = team; p < a.n; p += a.teams) {
+        problem_begin(a.probs + p, p, mmax);
+        PC q = load_pc();
+        if constexpr (!TEAM) q.G = 1;
+        q.use_ratio = RATIO ? 1 : 0;
+        if constexpr (VAR == VAR_GM) q.loss = FMPNP_GEMAN_MCCLURE;
+        q.bilinear = VAR == VAR_BILINEAR ? 1 : 0;
+        long long ngath = 0;  // texel gathers of this wave for this problem
+        while (!st.done) {
+            // project, gather, loss (+ partials)
+            const double lmax = eval_pass<T, WPS == WPS_LATENCY>(q, mmax, ngath);
+            if (q.use_ratio) {
+                if (!ratio_exchange(lmax)) break;
+                contrib_pass(q, mmax);
+            }
+            if (TEAM) team_arrive();
+            else __syncthreads();
+            if (tid < 64 && (!TEAM || team_wait())) {
+                dbg_stamp(q.stamps, 3);  // slowest wave + exchange
+                const double tot = combine_final_wave(mmax, TEAM);
+                dbg_stamp(q.stamps, 4);
+                lm_update_wave(tot, q.stamps);
+            }
+            __syncthreads();
+            dbg_stamp(q.stamps, 7);  // pose update + barrier
+            if (st.abort_flag) break;
+        }
+        // every wave of every team member adds its share (results are zeroed by the launcher)
+        if ((tid & 63) == 0 && ngath)
+            atomicAdd(reinterpret_cast<unsigned long long *>(&a.results[p].texel_gathers),
+                      (unsigned long long)ngath);
+        problem_end();
+    }
+    if (stamps_on && (tid & 63) == 0)
+        for (int k = 0; k < NSTAMP; ++k)
+            a.stamps[((size_t)blockIdx.x * (NT / 64) + (tid >> 6)) * NSTAMP + k] = st.stamp_ph[tid >> 6][k];
+}
+
+}  // namespace fmpnp

@@ -33,7 +33,7 @@ class sparseFeaturePnP(nn.Module):
     :216-243 (compute_cost), :245-494 (forward)."""
 
     def __init__(self, n_iters, loss_fn=_losses.squared_loss, lambda_=0.01, verbose=False, ratio_threshold=None,
-                 useGPU=False, storage=None, device=None, wgs_per_problem=0):
+                 useGPU=False, storage=None, device=None, wgs_per_problem=0, sampling="nearest"):
         super().__init__()
         self.iterations = n_iters
         self.loss_fn = loss_fn
@@ -47,6 +47,7 @@ class sparseFeaturePnP(nn.Module):
         self.storage = storage
         self.device = device
         self.wgs_per_problem = wgs_per_problem
+        self.sampling = sampling  # extension: "bilinear" samples 2x2 taps (the reference: "nearest")
         self.status_ = None
         self.last_result_ = None
 
@@ -71,7 +72,7 @@ class sparseFeaturePnP(nn.Module):
         code, alpha = _losses.resolve(self.loss_fn) if loss is None else (loss, 0.0)
         return _rf.make_options(self.iterations, self.lambda_, code, alpha,
                                 self.ratio_threshold_ if self.use_ratio_test_ else None, storage_code, mode,
-                                self.wgs_per_problem)
+                                self.wgs_per_problem, sampling=self.sampling)
 
     def _storage_for(self, fmap):
         if self.storage is not None:

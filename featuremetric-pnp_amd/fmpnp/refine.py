@@ -182,8 +182,15 @@ def make_problem(feats, fref, pts3d, K, im_width, im_height, R0, t0, c_begin=0, 
     return Problem(feats, fref.contiguous(), pts, K, im_width, im_height, R0, t0, c_begin, c_end)
 
 
+_SAMPLING = {"nearest": _lib.NEAREST, "bilinear": _lib.BILINEAR}
+
+
 def make_options(n_iters, lambda0=0.01, loss=_lib.SQUARED, barron_alpha=0.0, ratio_threshold=None,
-                 dtype=_lib.F32, mode=_lib.MODE_FORWARD, wgs_per_problem=0, max_teams=0, memoize=True):
+                 dtype=_lib.F32, mode=_lib.MODE_FORWARD, wgs_per_problem=0, max_teams=0, memoize=True,
+                 sampling="nearest"):
+    """fmpnp_options.  sampling: "nearest" (the reference's indexing_, model.py:74-97) or
+    "bilinear" (extension: 2x2 taps of f, gx, gy; definition in fmpnp_device.h bilinear_taps,
+    checked against the oracle's restatement -- no reference counterpart, parity unpinned)."""
     o = _lib.Options()
     o.mode = int(mode)
     o.n_iters = int(n_iters)
@@ -192,7 +199,7 @@ def make_options(n_iters, lambda0=0.01, loss=_lib.SQUARED, barron_alpha=0.0, rat
     o.ratio_threshold = 0.0 if ratio_threshold is None else float(ratio_threshold)
     o.loss = int(loss)
     o.barron_alpha = float(barron_alpha)
-    o.sampling = _lib.NEAREST
+    o.sampling = _SAMPLING[sampling] if isinstance(sampling, str) else int(sampling)
     o.dtype = int(dtype)
     o.wgs_per_problem = int(wgs_per_problem)
     o.max_teams = int(max_teams)

@@ -97,8 +97,9 @@ static void transform(const double R[9], const double t[3], const double X[3], d
 }
 
 /* p = round(K P / P_z) - 1 as int, then the mask (model.py:306-311,99-117).
- * Returns 1 if supported; *x,*y are the image pixel indices. */
-static int project(const double K[9], const double P[3], int W, int H, long *x, long *y)
+ * Returns 1 if supported; *x,*y are the image pixel indices, *qx,*qy the
+ * unrounded K P / P_z (used by the bilinear extension). */
+static int project(const double K[9], const double P[3], int W, int H, long *x, long *y, double *qx, double *qy)
 {
     double u[3];
     for (int i = 0; i < 3; ++i) {
@@ -107,8 +108,10 @@ static int project(const double K[9], const double P[3], int W, int H, long *x, 
         s = s + K[3 * i + 2] * P[2];
         u[i] = s;
     }
-    double px = rint(u[0] / u[2]) - 1.0; /* torch.round: half to even */
-    double py = rint(u[1] / u[2]) - 1.0;
+    *qx = u[0] / u[2];
+    *qy = u[1] / u[2];
+    double px = rint(*qx) - 1.0; /* torch.round: half to even */
+    double py = rint(*qy) - 1.0;
     /* int32 cast of a non-finite / out-of-range value lands outside [0,W) in
      * the reference (INT_MIN - 1 wraps); here the test on the double is
      * equivalent for every value that can be inside the image. */
@@ -116,6 +119,49 @@ static int project(const double K[9], const double P[3], int W, int H, long *x, 
     *x = (long)px;
     *y = (long)py;
     return 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Bilinear sampling (EXTENSION, not in the reference: its indexing_ is      */
+/* nearest-texel).  Definition shared bit-for-bit with the HIP kernel        */
+/* (fmpnp_device.h bilinear_taps):                                           */
+/*   sx = ((qx - 0.5) * Wf) / W - 0.5,  sy = ((qy - 0.5) * Hf) / H - 0.5     */
+/* (qx, qy = K P / P_z unrounded; the centre of image pixel index i, which   */
+/* the reference writes as round(q) - 1, is q = i + 1, and texel c's centre  */
+/* is sx = c), x0 = floor(sx), ax = sx - x0, taps at columns x0, x0 + 1 and  */
+/* rows y0, y0 + 1 clamped to the map, weights                               */
+/*   w00 = (1-ax)(1-ay), w01 = ax(1-ay), w10 = (1-ax)ay, w11 = ax ay,        */
+/* and every sampled value (f, gx, gy per channel) is                        */
+/*   fma(w11, v11, fma(w10, v10, fma(w01, v01, w00 * v00))).                 */
+/* The support set is the reference's (the rounded pixel inside the image).  */
+/* ------------------------------------------------------------------------ */
+typedef struct { long off[4]; double w[4]; } taps4;
+
+static void bilinear_taps(double qx, double qy, int Hf, int Wf, int im_w, int im_h, taps4 *tp)
+{
+    double sx = ((qx - 0.5) * (double)Wf) / (double)im_w - 0.5;
+    double sy = ((qy - 0.5) * (double)Hf) / (double)im_h - 0.5;
+    double fx0 = floor(sx), fy0 = floor(sy);
+    double ax = sx - fx0, ay = sy - fy0;
+    long x0 = (long)fx0, y0 = (long)fy0, x1 = x0 + 1, y1 = y0 + 1;
+    x0 = x0 < 0 ? 0 : (x0 > Wf - 1 ? Wf - 1 : x0);
+    x1 = x1 < 0 ? 0 : (x1 > Wf - 1 ? Wf - 1 : x1);
+    y0 = y0 < 0 ? 0 : (y0 > Hf - 1 ? Hf - 1 : y0);
+    y1 = y1 < 0 ? 0 : (y1 > Hf - 1 ? Hf - 1 : y1);
+    tp->off[0] = y0 * Wf + x0;
+    tp->off[1] = y0 * Wf + x1;
+    tp->off[2] = y1 * Wf + x0;
+    tp->off[3] = y1 * Wf + x1;
+    tp->w[0] = (1.0 - ax) * (1.0 - ay);
+    tp->w[1] = ax * (1.0 - ay);
+    tp->w[2] = (1.0 - ax) * ay;
+    tp->w[3] = ax * ay;
+}
+
+static double sample4(const double *plane_c, const taps4 *tp)
+{
+    return fma(tp->w[3], plane_c[tp->off[3]],
+               fma(tp->w[2], plane_c[tp->off[2]], fma(tp->w[1], plane_c[tp->off[1]], tp->w[0] * plane_c[tp->off[0]])));
 }
 
 /* ------------------------------------------------------------------------ */
@@ -131,7 +177,7 @@ typedef struct {
 
 static void evaluate(const orc_problem *pb, const orc_options *op, const double R[9], const double t[3],
                      int want_normal, eval_out *eo, double *rho_buf, unsigned char *sup_buf,
-                     double *err_buf, long *pix_buf)
+                     double *err_buf, long *pix_buf, taps4 *tap_buf)
 {
     const int N = pb->N, C = pb->C;
     const long plane = (long)pb->Hf * pb->Wf;
@@ -139,24 +185,34 @@ static void evaluate(const orc_problem *pb, const orc_options *op, const double 
     /* pass 1: projection, gather, residual, rho */
     double rho_max = 0.0;
     int first = 1;
+    const int bil = op->sampling == ORC_BILINEAR;
     for (int n = 0; n < N; ++n) {
-        double P[3];
+        double P[3], qx, qy;
         long x, y;
         transform(R, t, pb->pts + 3 * n, P);
-        sup_buf[n] = (unsigned char)project(pb->K, P, pb->im_w, pb->im_h, &x, &y);
+        sup_buf[n] = (unsigned char)project(pb->K, P, pb->im_w, pb->im_h, &x, &y, &qx, &qy);
         if (!sup_buf[n]) continue;
         eo->n_supported++;
-        /* indexing_ (model.py:88-89): row = floor(y*Hf/H), col = floor(x*Wf/W) */
-        long row = (y * (long)pb->Hf) / pb->im_h;
-        long col = (x * (long)pb->Wf) / pb->im_w;
-        long off = row * pb->Wf + col;
-        pix_buf[n] = off;
         double s = 0.0;
         const double *fr = pb->fref + (long)n * pb->ld_ref;
-        for (int c = 0; c < C; ++c) {
-            double e = pb->fmap[c * plane + off] - fr[c];
-            err_buf[(long)n * C + c] = e;
-            s += e * e;
+        if (bil) {
+            bilinear_taps(qx, qy, pb->Hf, pb->Wf, pb->im_w, pb->im_h, &tap_buf[n]);
+            for (int c = 0; c < C; ++c) {
+                double e = sample4(pb->fmap + c * plane, &tap_buf[n]) - fr[c];
+                err_buf[(long)n * C + c] = e;
+                s += e * e;
+            }
+        } else {
+            /* indexing_ (model.py:88-89): row = floor(y*Hf/H), col = floor(x*Wf/W) */
+            long row = (y * (long)pb->Hf) / pb->im_h;
+            long col = (x * (long)pb->Wf) / pb->im_w;
+            long off = row * pb->Wf + col;
+            pix_buf[n] = off;
+            for (int c = 0; c < C; ++c) {
+                double e = pb->fmap[c * plane + off] - fr[c];
+                err_buf[(long)n * C + c] = e;
+                s += e * e;
+            }
         }
         double xcost = 0.5 * s, rho, d1;
         loss_eval(op->loss, op->barron_alpha, xcost, &rho, &d1);
@@ -191,11 +247,18 @@ static void evaluate(const orc_problem *pb, const orc_options *op, const double 
          * per point J^T e and J^T J summed over channels (einsum :397,403), then
          * scaled by rho' and summed over points (:398-399, :404-405). */
         const double *err = err_buf + (long)n * C;
-        long off = pix_buf[n];
+        long off = bil ? 0 : pix_buf[n];
         double gp[6] = {0, 0, 0, 0, 0, 0}, Hp[36];
         memset(Hp, 0, sizeof(Hp));
         for (int c = 0; c < C; ++c) {
-            double gxv = pb->gx[c * plane + off], gyv = pb->gy[c * plane + off];
+            double gxv, gyv;
+            if (bil) {
+                gxv = sample4(pb->gx + c * plane, &tap_buf[n]);
+                gyv = sample4(pb->gy + c * plane, &tap_buf[n]);
+            } else {
+                gxv = pb->gx[c * plane + off];
+                gyv = pb->gy[c * plane + off];
+            }
             double B[3], Jc[6];
             for (int m = 0; m < 3; ++m) B[m] = gxv * Jpx[0][m] + gyv * Jpx[1][m];
             for (int k = 0; k < 6; ++k) {
@@ -294,7 +357,11 @@ int orc_forward(const orc_problem *pb, const orc_options *op, orc_result *res, o
     unsigned char *sup = (unsigned char *)malloc(N > 0 ? N : 1);
     double *err = (double *)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1) * (C > 0 ? C : 1));
     long *pix = (long *)malloc(sizeof(long) * (N > 0 ? N : 1));
-    if (!rho_buf || !sup || !err || !pix) { free(rho_buf); free(sup); free(err); free(pix); return -1; }
+    taps4 *taps = (taps4 *)malloc(sizeof(taps4) * (N > 0 ? N : 1));
+    if (!rho_buf || !sup || !err || !pix || !taps) {
+        free(rho_buf); free(sup); free(err); free(pix); free(taps);
+        return -1;
+    }
 
     double R[9], t[3], Rb[9], tb[3];
     memcpy(R, pb->R0, sizeof(R));
@@ -314,7 +381,7 @@ int orc_forward(const orc_problem *pb, const orc_options *op, orc_result *res, o
 
     for (int i = 0; i < op->n_iters; ++i) {
         eval_out lin;
-        evaluate(pb, op, R, t, 1, &lin, rho_buf, sup, err, pix);
+        evaluate(pb, op, R, t, 1, &lin, rho_buf, sup, err, pix, taps);
         if (lin.n_supported == 0) { /* model.py:316-320: return the CURRENT pose */
             res->status = ORC_NO_SUPPORT;
             returned_current = 1;
@@ -360,7 +427,7 @@ int orc_forward(const orc_problem *pb, const orc_options *op, orc_result *res, o
         matmul3(dR, R, Rn); /* model.py:425-426 */
         for (int r = 0; r < 3; ++r) tn[r] = (dR[3 * r] * t[0] + dR[3 * r + 1] * t[1] + dR[3 * r + 2] * t[2]) + delta[r];
         eval_out tri;
-        evaluate(pb, op, Rn, tn, 0, &tri, rho_buf, sup, err, pix);
+        evaluate(pb, op, Rn, tn, 0, &tri, rho_buf, sup, err, pix, taps);
         if (tri.n_supported == 0) { /* model.py:441-445: return the CURRENT pose */
             res->status = ORC_NO_SUPPORT_TRIAL;
             returned_current = 1;
@@ -409,6 +476,7 @@ int orc_forward(const orc_problem *pb, const orc_options *op, orc_result *res, o
     free(sup);
     free(err);
     free(pix);
+    free(taps);
     return 0;
 }
 
@@ -428,7 +496,7 @@ double orc_compute_cost(const orc_problem *pb, double ratio_threshold, const dou
     double *err = (double *)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1) * (C > 0 ? C : 1));
     long *pix = (long *)malloc(sizeof(long) * (N > 0 ? N : 1));
     eval_out eo;
-    evaluate(pb, &op, R, t, 0, &eo, rho_buf, sup, err, pix);
+    evaluate(pb, &op, R, t, 0, &eo, rho_buf, sup, err, pix, NULL);
     free(rho_buf);
     free(sup);
     free(err);

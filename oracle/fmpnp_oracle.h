@@ -8,6 +8,7 @@ extern "C" {
 
 enum { ORC_SQUARED = 0, ORC_HUBER = 1, ORC_CAUCHY = 2, ORC_GEMAN_MCCLURE = 3, ORC_BARRON = 4 };
 enum { ORC_OK = 0, ORC_NO_SUPPORT = 1, ORC_NAN = 2, ORC_NO_SUPPORT_TRIAL = 4 };
+enum { ORC_NEAREST = 0, ORC_BILINEAR = 1 }; /* sampling: the reference's NN, or the bilinear extension */
 
 typedef struct {
     const double *fmap, *gx, *gy; /* [C][Hf][Wf] fp64 (already channel-sliced) */
@@ -27,6 +28,7 @@ typedef struct {
     double ratio_threshold;
     int loss;
     double barron_alpha;
+    int sampling;                 /* ORC_NEAREST (the reference) or ORC_BILINEAR (extension) */
 } orc_options;
 
 typedef struct {
