@@ -356,6 +356,26 @@ def test_cfg2_shape_against_oracle(storage):
     np.testing.assert_allclose(tr["cost"], otr["cost"], rtol=1e-9 if storage == torch.float64 else 1e-6)
 
 
+@pytest.mark.parametrize("storage", [torch.float32, torch.float64])
+def test_cfg5_shape_against_oracle(storage):
+    """BASELINE config 5 shape (N=2048, C=512, 480x640, Cauchy, robotcar_inlier_GN.gin): C > 64 V
+    takes the multi-round gather, and 2048 points exceed one workgroup's LDS (G >= 2)."""
+    inputs = synth.problem_inputs(2048, 512, 480, 640, seed=5, device=DEV)
+    n_iters = 5
+    ores, otr = _oracle_on(inputs, n_iters, loss="cauchy")
+    feats = rf.pack_features(inputs["fmap"], storage=storage, device=DEV)
+    prob = rf.make_problem(feats, inputs["fref"], inputs["pts3d"], inputs["K"], inputs["im_width"],
+                           inputs["im_height"], inputs["R0"], inputs["t0"])
+    (res,), (tr,) = rf.refine([prob], rf.make_options(n_iters, 0.01, _lib.CAUCHY, dtype=feats.dtype_code),
+                              trace=True)
+    assert _lib.last_launch()["wgs_per_problem"] >= 2
+    assert rot_angle(res["R"], ores["R"]) < 1e-4
+    assert np.linalg.norm(res["t"] - ores["t"]) < 1e-4
+    np.testing.assert_array_equal(tr["n_supported"], otr["n_supported"])
+    np.testing.assert_allclose(tr["cost"], otr["cost"], rtol=1e-9 if storage == torch.float64 else 1e-6)
+    del feats, prob
+
+
 def test_batch_of_synthetic_queries_and_dtype_f32():
     """A batch of cfg2-like queries (smaller maps) against per-query oracle runs."""
     probs, ins = [], []
