@@ -137,6 +137,7 @@ struct SbRow {
     static constexpr int UNITS = SB_CB * QPC / SB_NT;           // vectors per thread
     Tin v[UNITS][VE];
     Tin halo;
+    unsigned okm;     // FAST loads: bit i = unit i lies inside the map, bit 31 = the halo does
 };
 
 template <typename Tin, bool FAST>
@@ -147,33 +148,51 @@ __device__ __forceinline__ void sb_load(SbRow<Tin> &r, const Tin *__restrict__ s
     int yy = y;
     bool row_ok = (y >= 0 && y < H);
     if (!row_ok && replicate) { yy = y < 0 ? 0 : H - 1; row_ok = true; }
+    if constexpr (FAST) {
+        // straight-line: every lane issues its loads from a clamped (valid) address and
+        // zeroes what lies outside the map, so the loads are a fixed count the compiler's
+        // vmcnt bookkeeping can see across the row loop (stores of the current row need not
+        // drain before the prefetched row is used)
+        const int ys = min(max(yy, 0), H - 1);
+        unsigned okm = 0;
+#pragma unroll
+        for (int i = 0; i < R::UNITS; ++i) {
+            const int u = t + SB_NT * i, cc = u / R::QPC, q = u - cc * R::QPC;
+            const int c = c0 + cc;
+            okm |= (c < C && row_ok) ? (1u << i) : 0u;
+            const Tin *p = src + ((size_t)min(c, C - 1) * H + ys) * W + x0 + q * R::VE;
+            if constexpr (sizeof(Tin) == 4) {
+                const float4 w = *reinterpret_cast<const float4 *>(p);
+                r.v[i][0] = w.x; r.v[i][1] = w.y; r.v[i][2] = w.z; r.v[i][3] = w.w;
+            } else {
+                const double2 w = *reinterpret_cast<const double2 *>(p);
+                r.v[i][0] = w.x; r.v[i][1] = w.y;
+            }
+        }
+        const int th = t & (2 * SB_CB - 1);  // threads >= 128 repeat a load and drop it
+        const int cc = th >> 1, c = c0 + cc;
+        int x = (th & 1) ? x0 + SB_XW : x0 - 1;
+        bool ok = (x >= 0 && x < W);
+        if (!ok && replicate) { x = x < 0 ? 0 : W - 1; ok = true; }
+        r.halo = src[((size_t)min(c, C - 1) * H + ys) * W + min(max(x, 0), W - 1)];
+        okm |= (t < 2 * SB_CB && ok && c < C && row_ok) ? (1u << 31) : 0u;
+        r.okm = okm;  // the zeroing waits for sb_store: no use of the loaded values here
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < R::UNITS; ++i) {
         const int u = t + SB_NT * i, cc = u / R::QPC, q = u - cc * R::QPC;
         const int c = c0 + cc, xb = x0 + q * R::VE;
         const Tin *p = src + ((size_t)c * H + yy) * W + xb;
-        if (FAST && c < C && row_ok) {
-            if constexpr (sizeof(Tin) == 4) {
-                float4 w = *reinterpret_cast<const float4 *>(p);
-                r.v[i][0] = w.x; r.v[i][1] = w.y; r.v[i][2] = w.z; r.v[i][3] = w.w;
-            } else {
-                double2 w = *reinterpret_cast<const double2 *>(p);
-                r.v[i][0] = w.x; r.v[i][1] = w.y;
-            }
-        } else if (!FAST) {
 #pragma unroll
-            for (int k = 0; k < R::VE; ++k) {
-                int x = xb + k;
-                Tin val = 0;
-                if (c < C && row_ok) {
-                    if (x < W) val = p[k];
-                    else if (replicate) val = src[((size_t)c * H + yy) * W + (W - 1)];
-                }
-                r.v[i][k] = val;
+        for (int k = 0; k < R::VE; ++k) {
+            int x = xb + k;
+            Tin val = 0;
+            if (c < C && row_ok) {
+                if (x < W) val = p[k];
+                else if (replicate) val = src[((size_t)c * H + yy) * W + (W - 1)];
             }
-        } else {
-#pragma unroll
-            for (int k = 0; k < R::VE; ++k) r.v[i][k] = 0;
+            r.v[i][k] = val;
         }
     }
     r.halo = 0;
@@ -184,6 +203,7 @@ __device__ __forceinline__ void sb_load(SbRow<Tin> &r, const Tin *__restrict__ s
         if (!ok && replicate) { x = x < 0 ? 0 : W - 1; ok = true; }
         if (c < C && row_ok && ok) r.halo = src[((size_t)c * H + yy) * W + x];
     }
+    r.okm = ~0u;
 }
 
 template <typename Tin>
@@ -193,10 +213,11 @@ __device__ __forceinline__ void sb_store(const SbRow<Tin> &r, Tin *slot) {
 #pragma unroll
     for (int i = 0; i < R::UNITS; ++i) {
         const int u = t + SB_NT * i, cc = u / R::QPC, q = u - cc * R::QPC;
+        const bool ok = (r.okm >> i) & 1u;
 #pragma unroll
-        for (int k = 0; k < R::VE; ++k) slot[cc * SB_LD + 1 + q * R::VE + k] = r.v[i][k];
+        for (int k = 0; k < R::VE; ++k) slot[cc * SB_LD + 1 + q * R::VE + k] = ok ? r.v[i][k] : (Tin)0;
     }
-    if (t < 2 * SB_CB) slot[(t >> 1) * SB_LD + ((t & 1) ? SB_XW + 1 : 0)] = r.halo;
+    if (t < 2 * SB_CB) slot[(t >> 1) * SB_LD + ((t & 1) ? SB_XW + 1 : 0)] = (r.okm >> 31) ? r.halo : (Tin)0;
 }
 
 // Store one output element through the row-tile buffer descriptor: voffset is the lane's
@@ -282,21 +303,24 @@ __device__ __forceinline__ void sobel_pack_body(const Tin *__restrict__ chw, int
     sb_store<Tin>(r, ring + (y0 & 3) * SE);
     sb_load<Tin, FAST>(r, chw, C, H, W, c0, x0, y0 + 1, replicate);
     sb_store<Tin>(r, ring + ((y0 + 1) & 3) * SE);
-    if (y0 + 2 <= y1) sb_load<Tin, FAST>(r, chw, C, H, W, c0, x0, y0 + 2, replicate);
+    // Row loop.  The next row's loads are issued BEFORE this row's stores: vmcnt retires in
+    // issue order, so waiting for the loads then leaves this row's stores in flight (issued
+    // after them the loads would wait for every store).  Lanes past C store to an
+    // out-of-range voffset, which the buffer range check drops (no divergent branch).
+    const int voff_s = FAST ? (c < C ? voff : 0x40000000) : voff;
     for (int y = y0; y < y1; ++y) {
-        __syncthreads();  // rows y-1, y, y+1 in their slots; nobody reads slot (y+2)&3 any more
-        if (c < C) {
+        __syncthreads();  // rows y-1, y, y+1 in their slots; slot (y+2)&3 is free
+        const bool more = y + 2 <= y1;
+        if (more) sb_load<Tin, FAST>(r, chw, C, H, W, c0, x0, y + 2, replicate);
+        if (FAST || c < C) {
             const int lo = cc * SB_LD + run * SB_RUN;
             const Tin *rm = ring + ((y - 1) & 3) * SE + lo;
             const Tin *r0 = ring + (y & 3) * SE + lo;
             const Tin *rp = ring + ((y + 1) & 3) * SE + lo;
             const int soff0 = ((y - y0) * W + x0 + wrun * SB_RUN) * tstride;
-            sb_row<Tin, Tout, FAST, NORM, NTS>(rm, r0, rp, rsrc, voff, soff0, tstride, pstride, ncols);
+            sb_row<Tin, Tout, FAST, NORM, NTS>(rm, r0, rp, rsrc, voff_s, soff0, tstride, pstride, ncols);
         }
-        if (y + 2 <= y1) {
-            sb_store<Tin>(r, ring + ((y + 2) & 3) * SE);
-            if (y + 3 <= y1) sb_load<Tin, FAST>(r, chw, C, H, W, c0, x0, y + 3, replicate);
-        }
+        if (more) sb_store<Tin>(r, ring + ((y + 2) & 3) * SE);
     }
 }
 
