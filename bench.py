@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=128, help="queries per GPU")
     ap.add_argument("--wgs", type=int, default=0, help="workgroups per query (0 = auto)")
-    ap.add_argument("--cpu-sample", type=int, default=512, help="queries in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=1024, help="queries in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-extras", action="store_true", help="skip single-query / pack / CPU legs")
     ap.add_argument("--no-nomemo", action="store_true", help="skip the memoisation-off comparison launch")
