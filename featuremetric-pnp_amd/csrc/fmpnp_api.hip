@@ -178,12 +178,26 @@ int fmpnp_pack_features(const void *chw, const void *gx_chw, const void *gy_chw,
                             sobel_replicate_pad, (hipStream_t)hip_stream);
 }
 
+static bool gather_args_ok(const void *ref_chw, int C, int H_ref, int W_ref, const double *ref_inliers, int N,
+                           int img0, int img1, const void *out, int ld_out) {
+    return ref_chw && ref_inliers && out && C > 0 && H_ref > 0 && W_ref > 0 && N > 0 && ld_out >= C && img0 > 0 &&
+           img1 > 0;
+}
+
+int fmpnp_gather_reference_async(const void *ref_chw, int dtype_in, int C, int H_ref, int W_ref,
+                                 const double *ref_inliers, int N, int img0, int img1, void *out, int dtype_out,
+                                 int ld_out, int *err_flag, void *hip_stream) {
+    if (N == 0) return 0;
+    if (!err_flag || !gather_args_ok(ref_chw, C, H_ref, W_ref, ref_inliers, N, img0, img1, out, ld_out))
+        return FMPNP_EINVAL;
+    return (int)launch_gather_ref(ref_chw, dtype_in, C, H_ref, W_ref, ref_inliers, N, img0, img1, out, dtype_out,
+                                  ld_out, err_flag, (hipStream_t)hip_stream);
+}
+
 int fmpnp_gather_reference(const void *ref_chw, int dtype_in, int C, int H_ref, int W_ref, const double *ref_inliers,
                            int N, int img0, int img1, void *out, int dtype_out, int ld_out, void *hip_stream) {
     if (N == 0) return 0;
-    if (!ref_chw || !ref_inliers || !out || C <= 0 || H_ref <= 0 || W_ref <= 0 || N < 0 || ld_out < C || img0 <= 0 ||
-        img1 <= 0)
-        return FMPNP_EINVAL;
+    if (!gather_args_ok(ref_chw, C, H_ref, W_ref, ref_inliers, N, img0, img1, out, ld_out)) return FMPNP_EINVAL;
     hipStream_t s = (hipStream_t)hip_stream;
     int *err = nullptr;
     hipError_t e = hipMallocAsync((void **)&err, sizeof(int), s);

@@ -1,0 +1,144 @@
+"""Streamed batch refinement: feature preparation of batch i+1 overlaps the LM launch of
+batch i on a second HIP stream.
+
+The per-query preparation of `feature_pnp` (optimize_feature_pnp.py:50-71 -> the fused
+Sobel + channels-last pack and the reference-descriptor gather) streams every query's
+hypercolumn through HBM once -- bandwidth-bound -- while the LM launch over a batch is
+latency-bound and reads little.  `RefinePipeline` runs the preparation on a `prep`
+stream and the LM launches on a `solve` stream, ordered by events:
+
+  * the packed maps of a batch live in one of `depth` slabs (a ring, reused across
+    batches and grown only when a batch needs more); the prep stream waits on the
+    event of the launch that last read a slab before packing into it again, so slab
+    reuse never blocks the host;
+  * every query's reference inliers and 3D points go up in one pinned, asynchronous
+    copy; out-of-map inliers (the reference's IndexError, optimize_feature_pnp.py:56)
+    set a per-query device flag that is checked when the batch's results are read,
+    so preparing a batch never waits for the device;
+  * the host runs at most `depth` batches ahead of the results it has collected.
+
+Results equal launching every batch alone (same kernels, same inputs; only the stream
+placement differs).  A query is (query_hc [C,H,W] or [1,C,H,W] device tensor,
+reference_hc, prediction, K) with the reference's `Prediction` fields (points_3d,
+reference_inliers, matrix).
+"""
+import numpy as np
+import torch
+
+from . import _lib, config
+from . import losses as _losses
+from . import refine as _rf
+
+_ALIGN = 256          # byte alignment of each packed map inside a slab
+_STREAMS = {}         # device index -> (prep, solve): shared so the allocator's per-stream pools are reused
+
+
+def _streams(device):
+    if device.index not in _STREAMS:
+        _STREAMS[device.index] = (torch.cuda.Stream(device), torch.cuda.Stream(device))
+    return _STREAMS[device.index]
+
+
+class RefinePipeline:
+    def __init__(self, image_shape=None, storage=torch.float32, device=None, depth=2, model_kwargs=None,
+                 sampling="nearest"):
+        cfg = config.adapter_kwargs()
+        self.image_shape = tuple(image_shape or cfg.get("image_shape", (1024, 1024)))
+        self.storage = storage
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        _lib.require_device(self.device)
+        kw = config.model_kwargs()
+        kw.update(model_kwargs or {})
+        loss_code, alpha = _losses.resolve(kw["loss_fn"])
+        self.options = _rf.make_options(kw["n_iters"], kw["lambda_"], loss_code, alpha, kw.get("ratio_threshold"),
+                                        _rf._dtype_code(storage), sampling=sampling)
+        self.depth = max(1, int(depth))
+        self.prep, self.solve = _streams(self.device)
+        self.slabs = [None] * self.depth        # flat uint8 device buffers holding a batch's packed maps
+        self.slab_free = [None] * self.depth    # event: the last launch that read the slab finished
+
+    def _slab(self, k, nbytes):
+        """Slab k with room for nbytes, usable on the prep stream once its last reader finished."""
+        if self.slab_free[k] is not None:
+            self.prep.wait_event(self.slab_free[k])
+        if self.slabs[k] is None or self.slabs[k].numel() < nbytes:
+            self.slabs[k] = None
+            with torch.cuda.stream(self.prep):
+                self.slabs[k] = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        return self.slabs[k]
+
+    def _prepare(self, queries, k):
+        """Pack + gather every query of a batch on the prep stream into slab k."""
+        es = torch.empty(0, dtype=self.storage).element_size()
+        shapes = []
+        for (q_hc, _, _, _) in queries:
+            C, H, W = q_hc.shape[-3:]
+            shapes.append((H, W, 3, _rf._round4(C)))
+        sizes = [int(np.prod(s)) * es for s in shapes]
+        starts = np.concatenate([[0], np.cumsum([(b + _ALIGN - 1) // _ALIGN * _ALIGN for b in sizes])])
+        probs = []
+        with torch.cuda.device(self.device), torch.cuda.stream(self.prep):
+            slab = self._slab(k, max(int(starts[-1]), 1))
+            # one out-of-map flag per query, read once the batch finished (no host wait here)
+            err = torch.zeros(len(queries), dtype=torch.int32, device=self.device)
+            # every query's reference inliers and 3D points in one pinned upload
+            inl = [np.asarray(p.reference_inliers, np.float64).reshape(-1, 2) for (_, _, p, _) in queries]
+            pts = [np.asarray(p.points_3d, np.float64).reshape(-1, 3) for (_, _, p, _) in queries]
+            flat = np.concatenate([a.reshape(-1) for a in inl + pts]) if queries else np.zeros(0)
+            dflat = torch.from_numpy(flat).pin_memory().to(self.device, non_blocking=True)
+            offs = np.concatenate([[0], np.cumsum([a.size for a in inl + pts])])
+            nq = len(queries)
+            for i, (q_hc, r_hc, pred, K) in enumerate(queries):
+                q = q_hc[0] if q_hc.dim() == 4 else q_hc
+                out = slab[int(starts[i]):int(starts[i]) + sizes[i]].view(self.storage).view(shapes[i])
+                feats = _rf.pack_features(q, storage=self.storage, device=self.device, out=out)  # :57, :61
+                fref = _rf.gather_reference(r_hc, dflat[offs[i]:offs[i + 1]].view(-1, 2), self.image_shape,
+                                            cstride=feats.cstride, storage=self.storage, device=self.device,
+                                            err_flag=err[i:i + 1])                              # :51-56
+                T = np.asarray(pred.matrix, dtype=np.float64)
+                probs.append(_rf.make_problem(feats, fref, dflat[offs[nq + i]:offs[nq + i + 1]].view(-1, 3),
+                                              np.asarray(K, np.float64).reshape(3, 3), self.image_shape[0],
+                                              self.image_shape[1], T[:3, :3], T[:3, 3]))     # :52, :59-60
+            batch = _rf.AsyncBatch(probs, self.options, non_blocking=True)
+        return batch, probs, err
+
+    def run(self, batches):
+        """batches: iterable of lists of queries.  Returns a list (per batch) of result dicts
+        (see refine.refine), computed with preparation and refinement overlapped."""
+        inflight = []   # (batch, probs, err flags, done event) in submission order
+        out = []
+
+        def finish(entry):
+            b, _, err, ev = entry
+            ev.synchronize()
+            bad = torch.nonzero(err.cpu()).flatten().tolist()
+            if bad:
+                raise IndexError(f"batch {len(out)}: reference inliers of queries {bad} map outside the reference "
+                                 "hypercolumn (optimize_feature_pnp.py:56 raises IndexError)")
+            out.append(b.results())
+
+        for i, queries in enumerate(batches):
+            # the host stays at most `depth` batches ahead of the collected results
+            while len(inflight) >= self.depth:
+                finish(inflight.pop(0))
+            k = i % self.depth
+            batch, probs, err = self._prepare(list(queries), k)
+            ready = torch.cuda.Event()
+            ready.record(self.prep)
+            self.solve.wait_event(ready)
+            with torch.cuda.device(self.device), torch.cuda.stream(self.solve):
+                batch.launch(_lib.stream_ptr(self.device))
+                # buffers written on the prep stream and read on the solve stream
+                for p in probs:
+                    p.fref.record_stream(self.solve)
+                    p.pts3d.record_stream(self.solve)
+                for t in (batch.d_descs, batch.d_res, batch.d_ws, err, self.slabs[k]):
+                    t.record_stream(self.solve)
+            done = torch.cuda.Event()
+            done.record(self.solve)
+            self.slab_free[k] = done
+            inflight.append((batch, probs, err, done))
+            del batch, probs, err
+        for entry in inflight:
+            finish(entry)
+        return out

@@ -45,15 +45,25 @@ class PackedFeatures:
         return _dtype_code(self.buf.dtype)
 
 
-def _as_device(x, device, dtype=None):
+def _as_device(x, device, dtype=None, non_blocking=False):
+    """Host or device array -> contiguous device tensor.  non_blocking: host data goes
+    through pinned memory and an asynchronous copy on the current stream (the host does
+    not wait for the device; torch's pinned allocator keeps the staging buffer alive
+    until the copy ran)."""
     t = x if isinstance(x, torch.Tensor) else torch.as_tensor(np.asarray(x))
-    t = t.to(device=device, dtype=dtype if dtype is not None else t.dtype)
+    dt = dtype if dtype is not None else t.dtype
+    if non_blocking and not t.is_cuda:
+        return t.to(dtype=dt).contiguous().pin_memory().to(device=device, non_blocking=True)
+    t = t.to(device=device, dtype=dt)
     return t.contiguous()
 
 
 def pack_features(fmap, gx=None, gy=None, storage=None, device=None, sobel_normalized=False,
-                  sobel_replicate_pad=False, stream=None):
+                  sobel_replicate_pad=False, stream=None, out=None):
     """[C,H,W] (or [1,C,H,W]) feature map -> PackedFeatures.
+
+    out: optional caller-owned contiguous device tensor [H, W, 3, cstride] of the
+    storage dtype to pack into (cstride = C rounded up to 4; a padded one is zeroed first).
 
     Without gx/gy the Sobel gradients are computed on the device (fused kernel;
     vendored kornia Sobel by default: unnormalised, zero padded,
@@ -80,8 +90,16 @@ def pack_features(fmap, gx=None, gy=None, storage=None, device=None, sobel_norma
                              device, in_dt)
             gyd = _as_device(gy.reshape(C, H, W) if isinstance(gy, torch.Tensor) else np.asarray(gy).reshape(C, H, W),
                              device, in_dt)
-        out = torch.zeros((H, W, 3, cs), dtype=storage, device=device) if cs != C else \
-            torch.empty((H, W, 3, cs), dtype=storage, device=device)
+        if out is not None:
+            if (tuple(out.shape) != (H, W, 3, cs) or out.dtype != storage or out.device != device
+                    or not out.is_contiguous()):
+                raise ValueError(f"out must be a contiguous {storage} tensor [{H}, {W}, 3, {cs}] on {device}")
+            if cs != C:
+                out.zero_()
+        elif cs != C:
+            out = torch.zeros((H, W, 3, cs), dtype=storage, device=device)
+        else:
+            out = torch.empty((H, W, 3, cs), dtype=storage, device=device)
         s = stream if stream is not None else _lib.stream_ptr(device)
         rc = _lib.load().fmpnp_pack_features(
             ctypes.c_void_p(f.data_ptr()), ctypes.c_void_p(gxd.data_ptr()) if gxd is not None else None,
@@ -104,8 +122,13 @@ def pad_reference(fref, cstride, storage, device):
     return out
 
 
-def gather_reference(ref_hc, reference_inliers, image_shape, cstride=None, storage=torch.float32, device=None):
-    """Device fref gather of optimize_feature_pnp.py:51-56 -> [N, cstride]."""
+def gather_reference(ref_hc, reference_inliers, image_shape, cstride=None, storage=torch.float32, device=None,
+                     err_flag=None):
+    """Device fref gather of optimize_feature_pnp.py:51-56 -> [N, cstride].
+
+    err_flag (a device int32 tensor of one element, zeroed by the caller): asynchronous
+    form -- nothing waits for the device, an out-of-map inlier sets the flag (checked by
+    the caller later) instead of raising here."""
     if ref_hc.dim() == 4:
         ref_hc = ref_hc[0]
     C, Hr, Wr = ref_hc.shape
@@ -116,10 +139,22 @@ def gather_reference(ref_hc, reference_inliers, image_shape, cstride=None, stora
     cs = cstride or _round4(C)
     with torch.cuda.device(device):
         ref = _as_device(ref_hc, device, in_dt)
-        inl = _as_device(torch.as_tensor(np.asarray(reference_inliers, dtype=np.float64).reshape(-1, 2)), device,
-                         torch.float64)
+        if isinstance(reference_inliers, torch.Tensor) and reference_inliers.is_cuda:
+            inl = reference_inliers.to(device=device, dtype=torch.float64).reshape(-1, 2).contiguous()
+        else:
+            inl = _as_device(torch.as_tensor(np.asarray(reference_inliers, dtype=np.float64).reshape(-1, 2)), device,
+                             torch.float64, non_blocking=err_flag is not None)
         N = inl.shape[0]
         out = torch.zeros((N, cs), dtype=storage, device=device)
+        if err_flag is not None:
+            if not (err_flag.is_cuda and err_flag.dtype == torch.int32):
+                raise TypeError("err_flag must be a device int32 tensor")
+            rc = _lib.load().fmpnp_gather_reference_async(
+                ctypes.c_void_p(ref.data_ptr()), _dtype_code(in_dt), C, Hr, Wr, ctypes.c_void_p(inl.data_ptr()), N,
+                int(image_shape[0]), int(image_shape[1]), ctypes.c_void_p(out.data_ptr()), _dtype_code(storage), cs,
+                ctypes.c_void_p(err_flag.data_ptr()), _lib.stream_ptr(device))
+            _lib.check(rc, "fmpnp_gather_reference_async")
+            return out
         rc = _lib.load().fmpnp_gather_reference(
             ctypes.c_void_p(ref.data_ptr()), _dtype_code(in_dt), C, Hr, Wr, ctypes.c_void_p(inl.data_ptr()), N,
             int(image_shape[0]), int(image_shape[1]), ctypes.c_void_p(out.data_ptr()), _dtype_code(storage), cs,
@@ -170,10 +205,11 @@ class Problem:
         return p
 
 
-def make_problem(feats, fref, pts3d, K, im_width, im_height, R0, t0, c_begin=0, c_end=None):
+def make_problem(feats, fref, pts3d, K, im_width, im_height, R0, t0, c_begin=0, c_end=None, non_blocking=False):
     dev = feats.buf.device
     pts = _as_device(torch.as_tensor(np.asarray(pts3d.detach().cpu() if isinstance(pts3d, torch.Tensor) else pts3d,
-                                                dtype=np.float64)).reshape(-1, 3), dev, torch.float64) \
+                                                dtype=np.float64)).reshape(-1, 3), dev, torch.float64,
+                     non_blocking) \
         if not (isinstance(pts3d, torch.Tensor) and pts3d.is_cuda and pts3d.dtype == torch.float64) \
         else pts3d.reshape(-1, 3).contiguous()
     if not (isinstance(fref, torch.Tensor) and fref.is_cuda and fref.dtype == feats.dtype
@@ -257,7 +293,7 @@ class AsyncBatch:
     """Device-resident descriptors/results/workspace for repeated asynchronous launches
     (the bench's timed region: nothing but the LM kernel and its counter memset)."""
 
-    def __init__(self, problems, options):
+    def __init__(self, problems, options, non_blocking=False):
         self.problems = list(problems)
         self.options = options
         n = len(self.problems)
@@ -269,7 +305,7 @@ class AsyncBatch:
         self.d_descs = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
         host = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(self.descs_host), nbytes)),
                                 dtype=torch.uint8)
-        self.d_descs.copy_(host)
+        self.d_descs.copy_(host.pin_memory() if non_blocking else host, non_blocking=non_blocking)
         self.d_res = torch.zeros(ctypes.sizeof(_lib.Result) * n, dtype=torch.uint8, device=self.dev)
         ws = _lib.load().fmpnp_workspace_size(self.descs_host, n, ctypes.byref(options))
         if ws == 0:

@@ -17,6 +17,7 @@
  *                                               optimize_feature_pnp.py:57,61
  *       (fused Sobel + channels-last [H][W][3][C] packing).
  *   fmpnp_gather_reference
+ *   fmpnp_gather_reference_async
  *       replaces the per-point fref gather       optimize_feature_pnp.py:51-56.
  *
  * Conventions: plain pointers and sizes, no torch types.  Feature / point
@@ -141,6 +142,15 @@ int fmpnp_pack_features(const void *chw, const void *gx_chw, const void *gy_chw,
 int fmpnp_gather_reference(const void *ref_chw, int dtype_in, int C, int H_ref, int W_ref,
                            const double *ref_inliers, int N, int img0, int img1, void *out, int dtype_out,
                            int ld_out, void *hip_stream);
+
+/* Asynchronous form of fmpnp_gather_reference: nothing is synchronised; an inlier
+ * outside the reference map ORs 1 into *err_flag (a device int the caller zeroes
+ * beforehand and reads after the stream reached this point) and zeroes its row.
+ * The batch pipeline (fmpnp.pipeline) uses it so preparing one batch never waits
+ * for the device. */
+int fmpnp_gather_reference_async(const void *ref_chw, int dtype_in, int C, int H_ref, int W_ref,
+                                 const double *ref_inliers, int N, int img0, int img1, void *out, int dtype_out,
+                                 int ld_out, int *err_flag, void *hip_stream);
 
 /* Device workspace needed by fmpnp_refine_batch_async for n problems. */
 size_t fmpnp_workspace_size(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt);

@@ -107,3 +107,66 @@ def test_batched_replay_reproduces_reference_feature_pnp():
         assert res["best_num_inliers"] == int(z["best_num_inliers_"])
     failed = [row for row in rows if row[2] is None]
     assert len(failed) == 1 and failed[0][1] == "query_5.jpg"
+
+
+@pytest.mark.gpu
+def test_pipeline_overlap_matches_golden_and_direct_launches():
+    """fmpnp.pipeline.RefinePipeline (prep stream || solve stream) over several batches gives
+    the reference's feature_pnp outputs for every query of every batch."""
+    import torch
+    import fmpnp
+    from fmpnp.pipeline import RefinePipeline
+    z, entries = golden_entries(n_ok=3, n_fail=0)
+    meta = json.loads(str(z["meta"]))
+    q = torch.from_numpy(z["in_query"]).to("cuda:0").double()
+    r = torch.from_numpy(z["in_ref"]).to("cuda:0").double()
+    pred = rp.prediction_from_entry(next(iter(entries.values())))
+    pipe = RefinePipeline(tuple(meta["image_shape"]), storage=torch.float64, depth=2,
+                          model_kwargs=dict(n_iters=meta["n_iters"], loss_fn=fmpnp.geman_mcclure_loss,
+                                            lambda_=meta["lambda0"], ratio_threshold=None))
+    batches = [[(q, r, pred, z["in_K"])] * nb for nb in (2, 3, 1, 4)]
+    out = pipe.run(batches)
+    assert [len(b) for b in out] == [2, 3, 1, 4]
+    for b in out:
+        for res in b:
+            np.testing.assert_allclose(res["R"], z["out_R"], atol=1e-9)
+            np.testing.assert_allclose(res["t"], z["out_t"], atol=1e-9)
+            assert res["best_num_inliers"] == int(z["best_num_inliers_"])
+
+
+@pytest.mark.gpu
+def test_gather_reference_async_matches_sync_and_flags_out_of_map():
+    import torch
+    from fmpnp import refine as rf
+    g = torch.Generator().manual_seed(3)
+    ref = torch.randn(37, 32, 32, generator=g).to("cuda:0")  # square: the reference swaps H and W scales
+    inl = np.stack([np.linspace(0, 1023, 50), np.linspace(1023, 0, 50)], 1)
+    a = rf.gather_reference(ref, inl, (1024, 1024), cstride=40)
+    err = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    b = rf.gather_reference(ref, inl, (1024, 1024), cstride=40, err_flag=err)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and int(err.item()) == 0
+    bad = inl.copy()
+    bad[7] = (2000.0, 5.0)   # row/col beyond the map -> the reference raises IndexError
+    with pytest.raises(IndexError):
+        rf.gather_reference(ref, bad, (1024, 1024), cstride=40)
+    rf.gather_reference(ref, bad, (1024, 1024), cstride=40, err_flag=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 1
+
+
+@pytest.mark.gpu
+def test_pipeline_raises_index_error_for_out_of_map_inliers():
+    import torch
+    import fmpnp
+    from fmpnp.pipeline import RefinePipeline
+    z, entries = golden_entries(n_ok=3, n_fail=0)
+    meta = json.loads(str(z["meta"]))
+    q = torch.from_numpy(z["in_query"]).to("cuda:0").double()
+    pred = rp.prediction_from_entry(next(iter(entries.values())))
+    r = torch.from_numpy(z["in_ref"]).to("cuda:0").double()
+    bad = pred._replace(reference_inliers=np.asarray(pred.reference_inliers) + 1e6)
+    pipe = RefinePipeline(tuple(meta["image_shape"]), storage=torch.float64,
+                          model_kwargs=dict(n_iters=3, loss_fn=fmpnp.geman_mcclure_loss))
+    with pytest.raises(IndexError):
+        pipe.run([[(q, r, pred, z["in_K"])], [(q, r, bad, z["in_K"])]])
