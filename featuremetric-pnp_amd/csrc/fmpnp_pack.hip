@@ -285,9 +285,9 @@ __device__ __forceinline__ void sb_row(const Tin *rm, const Tin *r0, const Tin *
 // FAST: 16-B vector loads (aligned rows) and all 32 tile columns inside the map.
 template <typename Tin, typename Tout, bool NORM, bool NTS, bool FAST>
 __device__ __forceinline__ void sobel_pack_body(const Tin *__restrict__ chw, int C, int H, int W, int cs, int rs,
-                                                int replicate, Tin *ring, __amdgpu_buffer_rsrc_t rsrc) {
+                                                int replicate, Tin *ring, __amdgpu_buffer_rsrc_t rsrc, int c0, int x0,
+                                                int y0) {
     constexpr int SE = SB_CB * SB_LD;
-    const int c0 = blockIdx.x * SB_CB, x0 = blockIdx.y * SB_XW, y0 = blockIdx.z * rs;
     const int y1 = min(y0 + rs, H);
     const int cc = threadIdx.x & 63, run = threadIdx.x >> 6;
     const int c = c0 + cc;
@@ -327,10 +327,26 @@ __device__ __forceinline__ void sobel_pack_body(const Tin *__restrict__ chw, int
 template <typename Tin, typename Tout, bool NORM, bool NTS>
 __global__ __launch_bounds__(SB_NT) void sobel_pack_kernel(const Tin *__restrict__ chw, int C, int H, int W,
                                                         Tout *__restrict__ out, int cs, int rs, int replicate,
-                                                        int vec_ok) {
+                                                        int vec_ok, int ncb, int nxw, int ntiles, int xcd_map) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Tin *ring = reinterpret_cast<Tin *>(smem);  // [SB_SLOTS][SB_CB][SB_LD]
-    const int x0 = blockIdx.y * SB_XW, y0 = blockIdx.z * rs;
+    // Tile order: channel chunk fastest, then column block, then row block.  xcd_map: the
+    // dispatcher deals consecutive workgroups round-robin over the 8 XCDs, so workgroup b
+    // takes tile (b % 8) * (grid / 8) + b / 8 -- each XCD gets one contiguous run of tiles
+    // (all channel chunks of a texel and the row/column neighbours that share halos go
+    // through the same L2).  The grid is padded to a multiple of 8; surplus groups exit.
+    const int b = blockIdx.x;
+    int t;
+    if (xcd_map == 2) {  // spatial tiles dealt round-robin over XCDs, all channel chunks of one together
+        const int j = b >> 3, s = (j / ncb) * 8 + (b & 7);
+        t = s * ncb + j % ncb;
+        if (s * ncb >= ntiles) return;
+    } else {
+        t = xcd_map ? (b & 7) * (int)(gridDim.x >> 3) + (b >> 3) : b;
+        if (t >= ntiles) return;
+    }
+    const int cb = t % ncb, xb = (t / ncb) % nxw, yb = t / (ncb * nxw);
+    const int c0 = cb * SB_CB, x0 = xb * SB_XW, y0 = yb * rs;
     const int y1 = min(y0 + rs, H);
     // descriptor over this tile's output rows [y0, y1) x all columns (byte offsets < 2^31)
     const size_t texel_elems = (size_t)3 * cs;
@@ -338,9 +354,9 @@ __global__ __launch_bounds__(SB_NT) void sobel_pack_kernel(const Tin *__restrict
     const unsigned tile_bytes = (unsigned)((size_t)(y1 - y0) * W * texel_elems * sizeof(Tout));
     __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_base, 0, tile_bytes, 0x00020000);
     if (vec_ok && x0 + SB_XW <= W)
-        sobel_pack_body<Tin, Tout, NORM, NTS, true>(chw, C, H, W, cs, rs, replicate, ring, rsrc);
+        sobel_pack_body<Tin, Tout, NORM, NTS, true>(chw, C, H, W, cs, rs, replicate, ring, rsrc, c0, x0, y0);
     else
-        sobel_pack_body<Tin, Tout, NORM, NTS, false>(chw, C, H, W, cs, rs, replicate, ring, rsrc);
+        sobel_pack_body<Tin, Tout, NORM, NTS, false>(chw, C, H, W, cs, rs, replicate, ring, rsrc, c0, x0, y0);
 }
 
 template <typename Tin, typename Tout>
@@ -361,7 +377,10 @@ static hipError_t pack_t(const void *chw, const void *gx, const void *gy, int C,
     if (rs < 4) rs = 4;
     nyb = (H + rs - 1) / rs;
     const int vec_ok = ((uintptr_t)chw % 16 == 0) && ((size_t)W * sizeof(Tin)) % 16 == 0;
-    dim3 grid(ncb, nxw, nyb);
+    const int ntiles = ncb * nxw * nyb;
+    static const int xcd_map = [] { const char *e = getenv("FMPNP_PACK_XCD"); return e ? atoi(e) : 1; }();
+    const int nsp = nxw * nyb;
+    dim3 grid(xcd_map == 2 ? (nsp + 7) / 8 * 8 * ncb : xcd_map ? (ntiles + 7) / 8 * 8 : ntiles);
     size_t lds = (size_t)SB_SLOTS * SB_CB * SB_LD * sizeof(Tin);
     // the output descriptor of a workgroup spans its rs rows: byte offsets must stay below 2^31
     if ((size_t)rs * W * 3 * cs * sizeof(Tout) >= ((size_t)1 << 31)) return hipErrorInvalidValue;
@@ -370,7 +389,7 @@ static hipError_t pack_t(const void *chw, const void *gx, const void *gy, int C,
     static const int nts = [] { const char *e = getenv("FMPNP_PACK_NT"); return !(e && *e == '0'); }();
 #define SB_LAUNCH(NORM, NTS)                                                                                    \
     hipLaunchKernelGGL((sobel_pack_kernel<Tin, Tout, NORM, NTS>), grid, dim3(SB_NT), lds, stream,              \
-                       (const Tin *)chw, C, H, W, (Tout *)out, cs, rs, replicate, vec_ok)
+                       (const Tin *)chw, C, H, W, (Tout *)out, cs, rs, replicate, vec_ok, ncb, nxw, ntiles, xcd_map)
     if (normalized) {
         if (nts) SB_LAUNCH(true, true); else SB_LAUNCH(true, false);
     } else {
