@@ -13,7 +13,8 @@ data path: ranks only meet in the timing barriers.
 
 Also reported: single-query latency (B=1, one query spread over several
 workgroups), the feature-pack kernel (fused Sobel + channels-last) rate, the
-roofline of the LM kernel, and the CPU baseline (the oracle's C restatement of
+end-to-end rate from CHW hypercolumns (pack + reference gather + LM through
+fmpnp.pipeline, wall clock), the roofline of the LM kernel, and the CPU baseline (the oracle's C restatement of
 the reference loop, OpenMP over queries) on a bounded sample.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
@@ -48,6 +49,7 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip single-query / pack / CPU legs")
     ap.add_argument("--no-nomemo", action="store_true", help="skip the memoisation-off comparison launch")
     ap.add_argument("--no-bilinear", action="store_true", help="skip the bilinear-sampling launch")
+    ap.add_argument("--no-pipeline", action="store_true", help="skip the end-to-end (pack + gather + LM) leg")
     return ap.parse_args()
 
 
@@ -309,6 +311,31 @@ def run_extras(args, dev, probs, keep, opts, rf, _lib, synth):
                    "frac_of_peak": round(pbytes / (pms / 1e3) / HBM_PEAK, 4),
                    "bytes_rule": "16C per texel (4C read + 12C written), %d distinct maps rotated" % NP}
     del fms, outs
+    # end to end from CHW hypercolumns (fmpnp.pipeline.RefinePipeline): pack + reference
+    # gather + LM per batch, preparation of batch i+1 on a second stream under batch i's LM
+    if not args.no_pipeline:
+        import fmpnp
+        from fmpnp.pipeline import RefinePipeline
+        nb, qb = 4, 32
+        batches, img = synth.pipeline_queries(nb, qb, N_PTS, C, HF, WF, device=dev, seed0=5000)
+        pipe = RefinePipeline(img, storage=torch.float32, depth=2,
+                              model_kwargs=dict(n_iters=ITERS, loss_fn=fmpnp.geman_mcclure_loss, lambda_=0.01,
+                                                ratio_threshold=None))
+        pipe.run(batches)  # sizes the slab ring
+        best = None
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            res = pipe.run(batches)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        out["end_to_end"] = {"queries_per_s": round(nb * qb / best, 1), "ms_per_query": round(best / (nb * qb) * 1e3, 4),
+                             "batches": nb, "batch": qb,
+                             "statuses": sorted({r["status"] for b in res for r in b}),
+                             "note": "wall clock, host included: Sobel+pack and reference gather of every "
+                                     "query (distinct maps) + one LM launch per batch, two streams"}
+        del batches, pipe
     # CPU baseline: the oracle (C restatement of the reference loop), OpenMP over queries
     if args.cpu_sample > 0 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         out["cpu_baseline"] = cpu_baseline(args, keep[0])

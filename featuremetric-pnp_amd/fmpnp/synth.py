@@ -9,6 +9,7 @@ reference descriptors = the nearest-texel gather at the identity pose, initial
 pose Rz(1 deg), t = (0.05, -0.03, 0.10).
 """
 import math
+from collections import namedtuple
 
 import numpy as np
 import torch
@@ -60,3 +61,33 @@ def problem_inputs(N=512, C=256, Hf=240, Wf=320, seed=0, device="cuda"):
     fref = reference_descriptors(fmap, X, K, W, H)
     return dict(fmap=fmap, fref=fref, pts3d=X, K=K, im_width=W, im_height=H, R0=rot_z(1.0),
                 t0=np.array([0.05, -0.03, 0.10]))
+
+
+# the reference's Prediction fields feature_pnp reads (s2dhm/pose_prediction/solve_pnp.py:7-8)
+QueryPrediction = namedtuple("QueryPrediction", "points_3d reference_inliers matrix")
+
+
+def pipeline_queries(n_batches, batch, N=512, C=256, Hf=240, Wf=320, device="cuda", seed0=0):
+    """Batches of feature_pnp-style queries (query_hc, reference_hc, prediction, K) for
+    fmpnp.pipeline.RefinePipeline, and the image_shape (W, H) they use.  The reference
+    hypercolumn is the query map; the reference inliers are placed so that the reference's
+    gather (optimize_feature_pnp.py:51-56: row = trunc(y * W_ref / image_shape[1]),
+    col = trunc(x * H_ref / image_shape[0])) picks each point's identity-pose texel, i.e.
+    the same descriptors as reference_descriptors()."""
+    batches = []
+    W, H = 4 * Wf, 4 * Hf
+    for b in range(n_batches):
+        qs = []
+        for i in range(batch):
+            seed = seed0 + 1000 * b + i
+            fmap = feature_map(C, Hf, Wf, seed, device)
+            X, K, _, _ = scene(N, Hf, Wf, seed)
+            p = project_pixels(np.eye(3), np.zeros(3), X, K)
+            rows = (p[:, 1].astype(np.int64) * Hf) // H
+            cols = (p[:, 0].astype(np.int64) * Wf) // W
+            inl = np.stack([(cols + 0.5) * W / Hf, (rows + 0.5) * H / Wf], 1)
+            T = np.eye(4)
+            T[:3, :3], T[:3, 3] = rot_z(1.0), np.array([0.05, -0.03, 0.10])
+            qs.append((fmap, fmap[None], QueryPrediction(X, inl, T), K))
+        batches.append(qs)
+    return batches, (W, H)

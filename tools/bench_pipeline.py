@@ -7,7 +7,6 @@ import json
 import os
 import sys
 import time
-from collections import namedtuple
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "featuremetric-pnp_amd")]
@@ -18,28 +17,10 @@ import fmpnp  # noqa: E402
 from fmpnp import synth  # noqa: E402
 from fmpnp.pipeline import RefinePipeline  # noqa: E402
 
-Pred = namedtuple("Pred", "points_3d reference_inliers matrix")
 NB = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 64
-N, C, H, W = 512, 256, 240, 320
 dev = torch.device("cuda", 0)
-img = (4 * W, 4 * H)  # (width, height) as the model reads image_shape[0], image_shape[1]
-
-batches = []
-for b in range(NB):
-    qs = []
-    for i in range(B):
-        inp = synth.problem_inputs(N, C, H, W, seed=1000 * b + i, device=dev)
-        # reference hypercolumn = the query map; reference inliers inside the region the
-        # reference's (row <- y*Wr/image_shape[1], col <- x*Hr/image_shape[0]) mapping keeps in range
-        K = inp["K"]
-        X = inp["pts3d"]
-        rng = np.random.default_rng(b * 7919 + i)
-        ref_inl = np.stack([rng.uniform(0, img[0], N), rng.uniform(0, img[1] * H / W, N)], 1)
-        T = np.eye(4)
-        T[:3, :3], T[:3, 3] = inp["R0"], inp["t0"]
-        qs.append((inp["fmap"], inp["fmap"][None], Pred(X, ref_inl, T), K))
-    batches.append(qs)
+batches, img = synth.pipeline_queries(NB, B, device=dev)
 torch.cuda.synchronize()
 kw = dict(n_iters=50, loss_fn=fmpnp.geman_mcclure_loss, lambda_=0.01, ratio_threshold=None)
 
