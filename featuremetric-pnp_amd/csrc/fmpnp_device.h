@@ -227,4 +227,62 @@ __device__ __forceinline__ double rlane64(double v, int l) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// An fp64 literal materialised where it is used: without this the compiler hoists the
+// 64-bit constants of the tail out of the problem loop into ~30 VGPRs that stay live (and
+// get spilled) through the point phase.  The volatile no-op pins the value to its use site
+// in an SGPR pair (two s_mov on the scalar unit).
+__host__ __device__ __forceinline__ double kc(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+s"(v));
+#endif
+    return v;
+}
+
+// sin, cos of 0 <= x <= pi/4 by Horner-form Taylor series to x^17 / x^18 (truncation
+// below 1e-19 relative; a few ulp of rounding): ~20 register-resident fp64 operations
+// instead of the library's range-reduced sincos on the LM tail's critical path.
+__host__ __device__ __forceinline__ void sincos_small(double x, double &s, double &c) {
+    const double z = x * x;
+    double ps = kc(1.0 / 355687428096000.0);
+    ps = fma(ps, z, kc(-1.0 / 1307674368000.0));
+    ps = fma(ps, z, kc(1.0 / 6227020800.0));
+    ps = fma(ps, z, kc(-1.0 / 39916800.0));
+    ps = fma(ps, z, kc(1.0 / 362880.0));
+    ps = fma(ps, z, kc(-1.0 / 5040.0));
+    ps = fma(ps, z, kc(1.0 / 120.0));
+    ps = fma(ps, z, kc(-1.0 / 6.0));
+    s = fma(x * z, ps, x);
+    double pc = kc(-1.0 / 6402373705728000.0);
+    pc = fma(pc, z, kc(1.0 / 20922789888000.0));
+    pc = fma(pc, z, kc(-1.0 / 87178291200.0));
+    pc = fma(pc, z, kc(1.0 / 479001600.0));
+    pc = fma(pc, z, kc(-1.0 / 3628800.0));
+    pc = fma(pc, z, kc(1.0 / 40320.0));
+    pc = fma(pc, z, kc(-1.0 / 720.0));
+    pc = fma(pc, z, kc(1.0 / 24.0));
+    pc = fma(pc, z, -0.5);
+    c = fma(z, pc, 1.0);
+}
+
+// sin, cos of a finite x > pi/4 (a rotation step of more than 45 degrees: rare): Cody-Waite
+// reduction by pi/2 (fdlibm's two-part constant, exact products for |n| < 2^20), then the
+// polynomial above on |r| <= pi/4 and the quadrant swap.  Replaces the library sincos,
+// whose table of 64-bit constants the compiler would otherwise hoist into registers that
+// stay live through the point phase.  Non-finite x gives NaN (as the library does).
+__host__ __device__ __forceinline__ void sincos_rr(double x, double &s, double &c) {
+    if (!(x < 1e300)) {
+        s = c = __builtin_nan("");
+        return;
+    }
+    const double n = rint(x * kc(6.36619772367581382433e-01));  // 2 / pi
+    double r = fma(-n, kc(1.57079632673412561417e+00), x);      // pio2_1 (33 bits)
+    r = fma(-n, kc(6.07710050650619224932e-11), r);             // pio2_1t
+    double sr, cr;
+    sincos_small(fabs(r), sr, cr);
+    if (r < 0.0) sr = -sr;
+    const int q = (int)(n - 4.0 * floor(n * 0.25));             // n mod 4, exact
+    s = q == 0 ? sr : (q == 1 ? cr : (q == 2 ? -sr : -cr));
+    c = q == 0 ? cr : (q == 1 ? -sr : (q == 2 ? -cr : sr));
+}
+
 }  // namespace fmpnp

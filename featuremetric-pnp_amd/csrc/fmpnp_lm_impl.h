@@ -165,32 +165,6 @@ __device__ __forceinline__ double *lds_part(int mmax) {
     return reinterpret_cast<double *>(dyn()) + (3 + RECW) * mmax + ((mmax + 3) / 4) * 2;
 }
 
-// sin, cos of 0 <= x <= pi/4 by Horner-form Taylor series to x^17 / x^18 (truncation
-// below 1e-19 relative; a few ulp of rounding): ~20 register-resident fp64 operations
-// instead of the library's range-reduced sincos on the LM tail's critical path.
-__device__ __forceinline__ void sincos_small(double x, double &s, double &c) {
-    const double z = x * x;
-    double ps = 1.0 / 355687428096000.0;
-    ps = fma(ps, z, -1.0 / 1307674368000.0);
-    ps = fma(ps, z, 1.0 / 6227020800.0);
-    ps = fma(ps, z, -1.0 / 39916800.0);
-    ps = fma(ps, z, 1.0 / 362880.0);
-    ps = fma(ps, z, -1.0 / 5040.0);
-    ps = fma(ps, z, 1.0 / 120.0);
-    ps = fma(ps, z, -1.0 / 6.0);
-    s = fma(x * z, ps, x);
-    double pc = -1.0 / 6402373705728000.0;
-    pc = fma(pc, z, 1.0 / 20922789888000.0);
-    pc = fma(pc, z, -1.0 / 87178291200.0);
-    pc = fma(pc, z, 1.0 / 479001600.0);
-    pc = fma(pc, z, -1.0 / 3628800.0);
-    pc = fma(pc, z, 1.0 / 40320.0);
-    pc = fma(pc, z, -1.0 / 720.0);
-    pc = fma(pc, z, 1.0 / 24.0);
-    pc = fma(pc, z, -0.5);
-    c = fma(z, pc, 1.0);
-}
-
 // so3exp_map (helpers/utils.py:209-221) and the update R' = dR R, t' = dR t + dt
 // (model.py:416-426).
 __device__ __forceinline__ void pose_update(const double *R, const double *t, const double delta[6], double *Rn,
@@ -207,7 +181,7 @@ __device__ __forceinline__ void pose_update(const double *R, const double *t, co
         const double W[9] = {0, -k2, k1, k2, 0, -k0, -k1, k0, 0};
         double s, c;
         if (theta <= 0.78539816339744828) sincos_small(theta, s, c);
-        else sincos(theta, &s, &c);
+        else sincos_rr(theta, s, c);
         const double c1 = 1.0 - c;
 #pragma unroll
         for (int i = 0; i < 3; ++i)

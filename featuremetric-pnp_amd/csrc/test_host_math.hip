@@ -1,0 +1,26 @@
+// Host check of the LM tail's sin/cos (fmpnp_device.h: sincos_small, sincos_rr) against
+// libm over the rotation-step range: prints the largest error in ulp-scaled units and exits
+// non-zero above the bound.  Built by the Makefile, run by tests/test_abi.py (CPU).
+#include <math.h>
+#include <stdio.h>
+
+#include "fmpnp_device.h"
+
+int main() {
+    double worst = 0.0, worst_x = 0.0;
+    const int n = 2000000;
+    for (int i = 0; i <= n; ++i) {
+        const double x = 200.0 * i / n;  // [0, 200] rad: 0..32 turns
+        double s, c;
+        if (x <= 0.78539816339744828) fmpnp::sincos_small(x, s, c);
+        else fmpnp::sincos_rr(x, s, c);
+        const double es = fabs(s - sin(x)), ec = fabs(c - cos(x));
+        const double e = fmax(es, ec) / 2.220446049250313e-16;  // in units of eps (|sin|, |cos| <= 1)
+        if (e > worst) { worst = e; worst_x = x; }
+    }
+    double s, c;
+    fmpnp::sincos_rr(INFINITY, s, c);
+    const bool nan_ok = isnan(s) && isnan(c);
+    printf("max error %.3f eps at x = %.17g; inf -> nan: %d\n", worst, worst_x, (int)nan_ok);
+    return (worst <= 8.0 && nan_ok) ? 0 : 1;
+}

@@ -73,3 +73,13 @@ def test_entry_points_reject_bad_arguments_without_a_device():
     o = _lib.Options()
     o.dtype = 7
     assert L.fmpnp_refine_batch(None, 1, ctypes.byref(o), None, None, 0, None) == -1
+
+
+def test_tail_sincos_matches_libm():
+    """The LM tail's polynomial sin/cos (fmpnp_device.h sincos_small / sincos_rr, which
+    replace the library sincos in so3exp_map, helpers/utils.py:209-221) stay within a few
+    eps of libm over 0..200 rad; non-finite angles give NaN.  Host build of the same code."""
+    pkg = os.path.join(ROOT, "featuremetric-pnp_amd")
+    subprocess.run(["make", "-s", "-C", pkg, "build/test_host_math"], check=True, timeout=300)
+    r = subprocess.run([os.path.join(pkg, "build", "test_host_math")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
