@@ -215,6 +215,48 @@ int fmpnp_gather_reference(const void *ref_chw, int dtype_in, int C, int H_ref, 
     return herr ? FMPNP_EINVAL : 0;  // an inlier outside the reference map (reference: IndexError)
 }
 
+int fmpnp_pack_features_batch(int n, const void *const *chw, void *const *out, const int *shape, int dtype_in,
+                              int dtype_out, int sobel_normalized, int sobel_replicate_pad, void *hip_stream) {
+    if (n < 0 || (n > 0 && (!chw || !out || !shape))) return FMPNP_EINVAL;
+    if ((dtype_in != FMPNP_F32 && dtype_in != FMPNP_F64) || (dtype_out != FMPNP_F32 && dtype_out != FMPNP_F64))
+        return FMPNP_EINVAL;
+    for (int i = 0; i < n; ++i) {  // every item checked before anything is launched
+        const int *sh = shape + 4 * i;
+        if (!chw[i] || !out[i] || sh[0] <= 0 || sh[1] <= 0 || sh[2] <= 0 || sh[3] < sh[0]) return FMPNP_EINVAL;
+    }
+    for (int i = 0; i < n; ++i) {
+        const int *sh = shape + 4 * i;
+        const hipError_t e = launch_pack(chw[i], nullptr, nullptr, dtype_in, sh[0], sh[1], sh[2], out[i], dtype_out,
+                                         sh[3], sobel_normalized, sobel_replicate_pad, (hipStream_t)hip_stream);
+        if (e != hipSuccess) return (int)e;
+    }
+    return 0;
+}
+
+int fmpnp_gather_reference_batch(int n, const void *const *ref_chw, const int *ref_shape,
+                                 const double *const *ref_inliers, const int *n_inliers, int img0, int img1,
+                                 void *const *out, const int *ld_out, int dtype_in, int dtype_out, int *err_flags,
+                                 void *hip_stream) {
+    if (n < 0 || (n > 0 && (!ref_chw || !ref_shape || !ref_inliers || !n_inliers || !out || !ld_out || !err_flags)))
+        return FMPNP_EINVAL;
+    for (int i = 0; i < n; ++i) {
+        const int *sh = ref_shape + 3 * i;
+        if (n_inliers[i] < 0) return FMPNP_EINVAL;
+        if (n_inliers[i] > 0 &&
+            !gather_args_ok(ref_chw[i], sh[0], sh[1], sh[2], ref_inliers[i], n_inliers[i], img0, img1, out[i], ld_out[i]))
+            return FMPNP_EINVAL;
+    }
+    for (int i = 0; i < n; ++i) {
+        if (n_inliers[i] == 0) continue;
+        const int *sh = ref_shape + 3 * i;
+        const hipError_t e = launch_gather_ref(ref_chw[i], dtype_in, sh[0], sh[1], sh[2], ref_inliers[i], n_inliers[i],
+                                               img0, img1, out[i], dtype_out, ld_out[i], err_flags + i,
+                                               (hipStream_t)hip_stream);
+        if (e != hipSuccess) return (int)e;
+    }
+    return 0;
+}
+
 size_t fmpnp_workspace_size(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt) {
     Plan P;
     if (make_plan(probs_host, n, opt, &P)) return 0;

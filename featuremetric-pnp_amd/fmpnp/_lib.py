@@ -52,7 +52,8 @@ class TraceEntry(ctypes.Structure):
 
 
 EXPORTS = ["fmpnp_abi_version", "fmpnp_build_info", "fmpnp_device_check", "fmpnp_pack_features",
-           "fmpnp_gather_reference", "fmpnp_gather_reference_async", "fmpnp_workspace_size", "fmpnp_refine_batch_async", "fmpnp_refine_batch",
+           "fmpnp_gather_reference", "fmpnp_gather_reference_async", "fmpnp_pack_features_batch",
+           "fmpnp_gather_reference_batch", "fmpnp_workspace_size", "fmpnp_refine_batch_async", "fmpnp_refine_batch",
            "fmpnp_last_launch", "fmpnp_debug_stamps"]
 
 _LIB = None
@@ -82,6 +83,10 @@ def load():
     L.fmpnp_gather_reference.restype = i
     L.fmpnp_gather_reference_async.argtypes = [vp, i, i, i, i, vp, i, i, i, vp, i, i, vp, vp]
     L.fmpnp_gather_reference_async.restype = i
+    L.fmpnp_pack_features_batch.argtypes = [i, vp, vp, vp, i, i, i, i, vp]
+    L.fmpnp_pack_features_batch.restype = i
+    L.fmpnp_gather_reference_batch.argtypes = [i, vp, vp, vp, vp, i, i, vp, vp, i, i, vp, vp]
+    L.fmpnp_gather_reference_batch.restype = i
     L.fmpnp_workspace_size.argtypes = [ctypes.POINTER(Problem), i, ctypes.POINTER(Options)]
     L.fmpnp_workspace_size.restype = ctypes.c_size_t
     L.fmpnp_refine_batch_async.argtypes = [vp, ctypes.POINTER(Problem), i, i, ctypes.POINTER(Options), vp, vp, i, vp,

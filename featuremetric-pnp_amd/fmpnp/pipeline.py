@@ -22,6 +22,8 @@ placement differs).  A query is (query_hc [C,H,W] or [1,C,H,W] device tensor,
 reference_hc, prediction, K) with the reference's `Prediction` fields (points_3d,
 reference_inliers, matrix).
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -68,39 +70,70 @@ class RefinePipeline:
         return self.slabs[k]
 
     def _prepare(self, queries, k):
-        """Pack + gather every query of a batch on the prep stream into slab k."""
-        es = torch.empty(0, dtype=self.storage).element_size()
-        shapes = []
-        for (q_hc, _, _, _) in queries:
-            C, H, W = q_hc.shape[-3:]
-            shapes.append((H, W, 3, _rf._round4(C)))
-        sizes = [int(np.prod(s)) * es for s in shapes]
-        starts = np.concatenate([[0], np.cumsum([(b + _ALIGN - 1) // _ALIGN * _ALIGN for b in sizes])])
+        """Pack + gather every query of a batch on the prep stream into slab k: one batched
+        C-ABI call each for the Sobel packs and the reference gathers (no per-query host
+        round trips)."""
+        dev, storage = self.device, self.storage
+        nq = len(queries)
+        qmaps = [q if q.dim() == 3 else q[0] for (q, _, _, _) in queries]
+        rmaps = [r if r.dim() == 3 else r[0] for (_, r, _, _) in queries]
+        q_dt = qmaps[0].dtype if qmaps and qmaps[0].dtype in (torch.float32, torch.float64) else torch.float32
+        r_dt = rmaps[0].dtype if rmaps and rmaps[0].dtype in (torch.float32, torch.float64) else torch.float32
+        es = torch.empty(0, dtype=storage).element_size()
+        shapes = [(m.shape[1], m.shape[2], 3, _rf._round4(m.shape[0])) for m in qmaps]
+        sizes = [int(np.prod(sh)) * es for sh in shapes]
+        starts = np.concatenate([[0], np.cumsum([(b + _ALIGN - 1) // _ALIGN * _ALIGN for b in sizes])]).astype(int)
+        inl = [np.asarray(p.reference_inliers, np.float64).reshape(-1, 2) for (_, _, p, _) in queries]
+        pts = [np.asarray(p.points_3d, np.float64).reshape(-1, 3) for (_, _, p, _) in queries]
+        n_pts = [a.shape[0] for a in inl]
         probs = []
-        with torch.cuda.device(self.device), torch.cuda.stream(self.prep):
+        with torch.cuda.device(dev), torch.cuda.stream(self.prep):
+            qmaps = [_rf._as_device(m, dev, q_dt) for m in qmaps]   # no-ops for device maps of the batch dtype
+            rmaps = [_rf._as_device(m, dev, r_dt) for m in rmaps]
             slab = self._slab(k, max(int(starts[-1]), 1))
+            outs = [slab[starts[i]:starts[i] + sizes[i]].view(storage).view(shapes[i]) for i in range(nq)]
+            for i in range(nq):
+                if shapes[i][3] != qmaps[i].shape[0]:
+                    outs[i].zero_()  # padding channels stay zero (the kernel writes c < C only)
             # one out-of-map flag per query, read once the batch finished (no host wait here)
-            err = torch.zeros(len(queries), dtype=torch.int32, device=self.device)
+            err = torch.zeros(nq, dtype=torch.int32, device=dev)
             # every query's reference inliers and 3D points in one pinned upload
-            inl = [np.asarray(p.reference_inliers, np.float64).reshape(-1, 2) for (_, _, p, _) in queries]
-            pts = [np.asarray(p.points_3d, np.float64).reshape(-1, 3) for (_, _, p, _) in queries]
-            flat = np.concatenate([a.reshape(-1) for a in inl + pts]) if queries else np.zeros(0)
-            dflat = torch.from_numpy(flat).pin_memory().to(self.device, non_blocking=True)
-            offs = np.concatenate([[0], np.cumsum([a.size for a in inl + pts])])
-            nq = len(queries)
-            for i, (q_hc, r_hc, pred, K) in enumerate(queries):
-                q = q_hc[0] if q_hc.dim() == 4 else q_hc
-                out = slab[int(starts[i]):int(starts[i]) + sizes[i]].view(self.storage).view(shapes[i])
-                feats = _rf.pack_features(q, storage=self.storage, device=self.device, out=out)  # :57, :61
-                fref = _rf.gather_reference(r_hc, dflat[offs[i]:offs[i + 1]].view(-1, 2), self.image_shape,
-                                            cstride=feats.cstride, storage=self.storage, device=self.device,
-                                            err_flag=err[i:i + 1])                              # :51-56
+            flat = np.concatenate([a.reshape(-1) for a in inl + pts]) if nq else np.zeros(0)
+            dflat = torch.from_numpy(flat).pin_memory().to(dev, non_blocking=True)
+            offs = np.concatenate([[0], np.cumsum([a.size for a in inl + pts])]).astype(int)
+            # reference descriptors of the whole batch: [N_i][cstride_i] runs in one buffer
+            fr_off = np.concatenate([[0], np.cumsum([n_pts[i] * shapes[i][3] for i in range(nq)])]).astype(int)
+            pad = any(shapes[i][3] != rmaps[i].shape[0] for i in range(nq))
+            fbuf = (torch.zeros if pad else torch.empty)(max(int(fr_off[-1]), 1), dtype=storage, device=dev)
+            frefs = [fbuf[fr_off[i]:fr_off[i + 1]].view(n_pts[i], shapes[i][3]) for i in range(nq)]
+            L = _lib.load()
+            vp = ctypes.c_void_p
+            s = _lib.stream_ptr(dev)
+            shape_arr = (ctypes.c_int * (4 * nq))(*[v for i in range(nq) for v in
+                                                    (qmaps[i].shape[0], shapes[i][0], shapes[i][1], shapes[i][3])])
+            rc = L.fmpnp_pack_features_batch(
+                nq, (vp * nq)(*[m.data_ptr() for m in qmaps]), (vp * nq)(*[o.data_ptr() for o in outs]), shape_arr,
+                _rf._dtype_code(q_dt), _rf._dtype_code(storage), 0, 0, s)                    # :57, :61
+            _lib.check(rc, "fmpnp_pack_features_batch")
+            rshape = (ctypes.c_int * (3 * nq))(*[v for m in rmaps for v in m.shape])
+            base = dflat.data_ptr()
+            rc = L.fmpnp_gather_reference_batch(
+                nq, (vp * nq)(*[m.data_ptr() for m in rmaps]), rshape,
+                (vp * nq)(*[base + 8 * int(offs[i]) for i in range(nq)]), (ctypes.c_int * nq)(*n_pts),
+                int(self.image_shape[0]), int(self.image_shape[1]), (vp * nq)(*[f.data_ptr() for f in frefs]),
+                (ctypes.c_int * nq)(*[sh[3] for sh in shapes]), _rf._dtype_code(r_dt), _rf._dtype_code(storage),
+                vp(err.data_ptr()), s)                                                        # :51-56
+            _lib.check(rc, "fmpnp_gather_reference_batch")
+            for i, (_, _, pred, K) in enumerate(queries):
+                feats = _rf.PackedFeatures(outs[i], qmaps[i].shape[0], shapes[i][0], shapes[i][1], shapes[i][3])
                 T = np.asarray(pred.matrix, dtype=np.float64)
-                probs.append(_rf.make_problem(feats, fref, dflat[offs[nq + i]:offs[nq + i + 1]].view(-1, 3),
+                probs.append(_rf.make_problem(feats, frefs[i], dflat[offs[nq + i]:offs[nq + i + 1]].view(-1, 3),
                                               np.asarray(K, np.float64).reshape(3, 3), self.image_shape[0],
                                               self.image_shape[1], T[:3, :3], T[:3, 3]))     # :52, :59-60
             batch = _rf.AsyncBatch(probs, self.options, non_blocking=True)
-        return batch, probs, err
+        # the maps are read on the prep stream only; keep them (and any converted copies)
+        # alive until the batch is collected
+        return batch, probs + [qmaps, rmaps, fbuf], err
 
     def run(self, batches):
         """batches: iterable of lists of queries.  Returns a list (per batch) of result dicts
@@ -130,8 +163,9 @@ class RefinePipeline:
                 batch.launch(_lib.stream_ptr(self.device))
                 # buffers written on the prep stream and read on the solve stream
                 for p in probs:
-                    p.fref.record_stream(self.solve)
-                    p.pts3d.record_stream(self.solve)
+                    if isinstance(p, _rf.Problem):
+                        p.fref.record_stream(self.solve)
+                        p.pts3d.record_stream(self.solve)
                 for t in (batch.d_descs, batch.d_res, batch.d_ws, err, self.slabs[k]):
                     t.record_stream(self.solve)
             done = torch.cuda.Event()

@@ -12,12 +12,12 @@
  *          indexing_ / points_within_image      featurePnP/model.py:74-117,
  *          ratio_threshold_feature_errors       featurePnP/model.py:120-129,
  *          so3exp_map                           featurePnP/helpers/utils.py:209-221.
- *   fmpnp_pack_features
+ *   fmpnp_pack_features / fmpnp_pack_features_batch
  *       replaces sobel_filter + the fp64 cast   featurePnP/helpers/utils.py:81-104,
  *                                               optimize_feature_pnp.py:57,61
  *       (fused Sobel + channels-last [H][W][3][C] packing).
  *   fmpnp_gather_reference
- *   fmpnp_gather_reference_async
+ *   fmpnp_gather_reference_async / fmpnp_gather_reference_batch
  *       replaces the per-point fref gather       optimize_feature_pnp.py:51-56.
  *
  * Conventions: plain pointers and sizes, no torch types.  Feature / point
@@ -151,6 +151,18 @@ int fmpnp_gather_reference(const void *ref_chw, int dtype_in, int C, int H_ref, 
 int fmpnp_gather_reference_async(const void *ref_chw, int dtype_in, int C, int H_ref, int W_ref,
                                  const double *ref_inliers, int N, int img0, int img1, void *out, int dtype_out,
                                  int ld_out, int *err_flag, void *hip_stream);
+
+/* Batched forms for a caller preparing many queries at once (fmpnp.pipeline): one host
+ * call, one launch per item on hip_stream, nothing synchronised.  Host arrays of n entries;
+ * shape[4*i..] = (C, H, W, cstride) of map i, ref_shape[3*i..] = (C, H_ref, W_ref) of
+ * reference map i; err_flags is a DEVICE int[n] the caller zeroes (set as in
+ * fmpnp_gather_reference_async).  Every item is validated before anything is launched. */
+int fmpnp_pack_features_batch(int n, const void *const *chw, void *const *out, const int *shape, int dtype_in,
+                              int dtype_out, int sobel_normalized, int sobel_replicate_pad, void *hip_stream);
+int fmpnp_gather_reference_batch(int n, const void *const *ref_chw, const int *ref_shape,
+                                 const double *const *ref_inliers, const int *n_inliers, int img0, int img1,
+                                 void *const *out, const int *ld_out, int dtype_in, int dtype_out, int *err_flags,
+                                 void *hip_stream);
 
 /* Device workspace needed by fmpnp_refine_batch_async for n problems. */
 size_t fmpnp_workspace_size(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt);
