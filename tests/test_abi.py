@@ -73,6 +73,21 @@ def test_entry_points_reject_bad_arguments_without_a_device():
     o = _lib.Options()
     o.dtype = 7
     assert L.fmpnp_refine_batch(None, 1, ctypes.byref(o), None, None, 0, None) == -1
+    assert L.fmpnp_gather_reference_async(None, 0, 1, 1, 1, None, 1, 1, 1, None, 0, 1, None, None) == -1
+    # batched forms: negative counts, missing arrays, and one bad item among good ones are
+    # refused before anything is launched
+    vp = ctypes.c_void_p
+    assert L.fmpnp_pack_features_batch(-1, None, None, None, 0, 0, 0, 0, None) == -1
+    assert L.fmpnp_pack_features_batch(1, None, None, None, 0, 0, 0, 0, None) == -1
+    assert L.fmpnp_pack_features_batch(0, None, None, None, 0, 0, 0, 0, None) == 0
+    two = (vp * 2)(1, 2)
+    shape = (ctypes.c_int * 8)(4, 2, 2, 4, 4, 2, 2, 3)  # item 1: cstride < C
+    assert L.fmpnp_pack_features_batch(2, two, two, shape, 0, 0, 0, 0, None) == -1
+    assert L.fmpnp_gather_reference_batch(1, None, None, None, None, 1, 1, None, None, 0, 0, None, None) == -1
+    rshape = (ctypes.c_int * 6)(4, 2, 2, 4, 2, 2)
+    n_in = (ctypes.c_int * 2)(3, -1)                    # item 1: negative point count
+    ld = (ctypes.c_int * 2)(4, 4)
+    assert L.fmpnp_gather_reference_batch(2, two, rshape, two, n_in, 8, 8, two, ld, 0, 0, vp(3), None) == -1
 
 
 def test_tail_sincos_matches_libm():
