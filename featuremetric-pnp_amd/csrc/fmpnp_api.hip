@@ -39,11 +39,17 @@ int validate(const fmpnp_problem *probs, int n, const fmpnp_options *opt) {
     if (opt->loss < FMPNP_SQUARED || opt->loss > FMPNP_BARRON) return FMPNP_EINVAL;
     if (opt->mode != FMPNP_MODE_FORWARD && opt->mode != FMPNP_MODE_COMPUTE_COST) return FMPNP_EINVAL;
     if (opt->sampling != FMPNP_NEAREST && opt->sampling != FMPNP_BILINEAR) return FMPNP_EINVAL;
+    if (opt->layout != FMPNP_LAYOUT_FGRAD && opt->layout != FMPNP_LAYOUT_F) return FMPNP_EINVAL;
+    // the f-only layout: fp32 texels, nearest sampling (the LM kernel's in-gather Sobel)
+    if (opt->layout == FMPNP_LAYOUT_F && (opt->dtype != FMPNP_F32 || opt->sampling != FMPNP_NEAREST))
+        return FMPNP_EINVAL;
+    if (opt->sobel_flags & ~3) return FMPNP_EINVAL;
     for (int i = 0; i < n; ++i) {
         const fmpnp_problem &p = probs[i];
         if (p.N < 0 || p.Hf <= 0 || p.Wf <= 0 || p.im_width <= 0 || p.im_height <= 0) return FMPNP_EINVAL;
         if (p.c_begin < 0 || p.c_end < p.c_begin || p.c_end > p.cstride || p.c_end > p.ld_ref) return FMPNP_EINVAL;
         if (p.N > 0 && (!p.feat || !p.fref || !p.pts3d)) return FMPNP_EINVAL;
+        if (opt->layout == FMPNP_LAYOUT_F && (p.Hf >= 65536 || p.Wf >= 65536)) return FMPNP_ETOOBIG;
         // every projected pixel maps to a texel < Hf*Wf; the packed map must hold 3*cstride per texel
         if ((long long)p.Hf * p.Wf * 3 * (long long)p.cstride > (1LL << 40)) return FMPNP_ETOOBIG;
         // pixel -> texel rescale in 32-bit unsigned arithmetic: y * Hf < 2^32, x * Wf < 2^32
@@ -117,7 +123,7 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     // planner uses it only on request (FMPNP_LM_WPS=4, a tuning knob)
     const char *wps_env = getenv("FMPNP_LM_WPS");
     const bool want_tp = wps_env && atoi(wps_env) == 4;
-    P.wps = (want_tp && G == 1 && (long)n >= 2L * ncu && 2 * P.lds <= lds_cu) ? WPS_THROUGHPUT : WPS_LATENCY;
+    P.wps = (want_tp && opt->layout == FMPNP_LAYOUT_FGRAD && G == 1 && (long)n >= 2L * ncu && 2 * P.lds <= lds_cu) ? WPS_THROUGHPUT : WPS_LATENCY;
     const int per_cu = occupancy(P.lds);
     long cap = (long)ncu * per_cu;
     if (G == 1) cap = std::max(cap, (long)n);  // no cross-workgroup waits: any grid is safe
@@ -215,9 +221,20 @@ int fmpnp_gather_reference(const void *ref_chw, int dtype_in, int C, int H_ref, 
     return herr ? FMPNP_EINVAL : 0;  // an inlier outside the reference map (reference: IndexError)
 }
 
+int fmpnp_pack_features_f(const void *chw, int dtype_in, int C, int H, int W, void *out, int dtype_out,
+                          int cstride, void *hip_stream) {
+    if (!chw || !out || C <= 0 || H <= 0 || W <= 0 || cstride < C) return FMPNP_EINVAL;
+    if ((dtype_in != FMPNP_F32 && dtype_in != FMPNP_F64) || (dtype_out != FMPNP_F32 && dtype_out != FMPNP_F64))
+        return FMPNP_EINVAL;
+    return (int)launch_pack(chw, nullptr, nullptr, dtype_in, C, H, W, out, dtype_out, cstride, 0, 0,
+                            (hipStream_t)hip_stream, 1);
+}
+
 int fmpnp_pack_features_batch(int n, const void *const *chw, void *const *out, const int *shape, int dtype_in,
-                              int dtype_out, int sobel_normalized, int sobel_replicate_pad, void *hip_stream) {
+                              int dtype_out, int sobel_normalized, int sobel_replicate_pad, int layout,
+                              void *hip_stream) {
     if (n < 0 || (n > 0 && (!chw || !out || !shape))) return FMPNP_EINVAL;
+    if (layout != FMPNP_LAYOUT_FGRAD && layout != FMPNP_LAYOUT_F) return FMPNP_EINVAL;
     if ((dtype_in != FMPNP_F32 && dtype_in != FMPNP_F64) || (dtype_out != FMPNP_F32 && dtype_out != FMPNP_F64))
         return FMPNP_EINVAL;
     for (int i = 0; i < n; ++i) {  // every item checked before anything is launched
@@ -227,7 +244,8 @@ int fmpnp_pack_features_batch(int n, const void *const *chw, void *const *out, c
     for (int i = 0; i < n; ++i) {
         const int *sh = shape + 4 * i;
         const hipError_t e = launch_pack(chw[i], nullptr, nullptr, dtype_in, sh[0], sh[1], sh[2], out[i], dtype_out,
-                                         sh[3], sobel_normalized, sobel_replicate_pad, (hipStream_t)hip_stream);
+                                         sh[3], sobel_normalized, sobel_replicate_pad, (hipStream_t)hip_stream,
+                                         layout == FMPNP_LAYOUT_F ? 1 : 3);
         if (e != hipSuccess) return (int)e;
     }
     return 0;

@@ -43,11 +43,13 @@ hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipSt
 // LM kernel variants (fmpnp_lm_impl.h): Geman-McClure forward with nearest sampling (the
 // hot path), any loss / mode with nearest sampling, bilinear sampling
 constexpr int VAR_NEAREST = 0, VAR_GM = 1, VAR_BILINEAR = 2;
+// ... and the same two nearest variants on FMPNP_LAYOUT_F maps (fp32 only)
+constexpr int VAR_F_NEAREST = 3, VAR_F_GM = 4;
 int lm_variant(const fmpnp_options &o);
 const void *lm_kernel_ptr(int dtype, int wps, bool team, bool ratio, int var);
 
 hipError_t launch_pack(const void *chw, const void *gx, const void *gy, int dtype_in, int C, int H, int W, void *out,
-                       int dtype_out, int cstride, int normalized, int replicate, hipStream_t stream);
+                       int dtype_out, int cs, int normalized, int replicate, hipStream_t stream, int planes = 3);
 hipError_t launch_gather_ref(const void *ref, int dtype_in, int C, int H, int W, const double *inl, int N, int img0,
                              int img1, void *out, int dtype_out, int ld_out, int *err, hipStream_t stream);
 

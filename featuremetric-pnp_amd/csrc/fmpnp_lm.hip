@@ -51,7 +51,9 @@ const void *lm_kernel_ptr(int dtype, int wps, bool team, bool ratio, int var) {
 
 int lm_variant(const fmpnp_options &o) {
     if (o.sampling == FMPNP_BILINEAR) return VAR_BILINEAR;
-    return (o.loss == FMPNP_GEMAN_MCCLURE && o.mode == FMPNP_MODE_FORWARD) ? VAR_GM : VAR_NEAREST;
+    const bool gm = o.loss == FMPNP_GEMAN_MCCLURE && o.mode == FMPNP_MODE_FORWARD;
+    if (o.layout == FMPNP_LAYOUT_F) return gm ? VAR_F_GM : VAR_F_NEAREST;
+    return gm ? VAR_GM : VAR_NEAREST;
 }
 
 hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream) {

@@ -9,6 +9,12 @@ template <int WPS, bool TEAM, bool RATIO>
 static LmFn pick_var(int var) {
     if (var == VAR_GM) return lm_kernel<float, WPS, TEAM, RATIO, VAR_GM>;
     if (var == VAR_BILINEAR) return lm_kernel<float, WPS, TEAM, RATIO, VAR_BILINEAR>;
+    if constexpr (WPS == WPS_LATENCY) {  // FMPNP_LAYOUT_F (the planner keeps it on the latency build)
+        if (var == VAR_F_GM) return lm_kernel<float, WPS, TEAM, RATIO, VAR_F_GM>;
+        if (var == VAR_F_NEAREST) return lm_kernel<float, WPS, TEAM, RATIO, VAR_F_NEAREST>;
+    } else {
+        if (var >= VAR_F_NEAREST) return nullptr;
+    }
     return lm_kernel<float, WPS, TEAM, RATIO, VAR_NEAREST>;
 }
 template <int WPS>

@@ -7,6 +7,7 @@ namespace fmpnp {
 typedef void (*LmFn)(LaunchArgs);
 template <int WPS, bool TEAM, bool RATIO>
 static LmFn pick_var(int var) {
+    if (var >= VAR_F_NEAREST) return nullptr;  // FMPNP_LAYOUT_F is fp32-only (validated)
     if (var == VAR_GM) return lm_kernel<double, WPS, TEAM, RATIO, VAR_GM>;
     if (var == VAR_BILINEAR) return lm_kernel<double, WPS, TEAM, RATIO, VAR_BILINEAR>;
     return lm_kernel<double, WPS, TEAM, RATIO, VAR_NEAREST>;

@@ -59,7 +59,7 @@ struct Ctx {
     double *part_g;       // [2][nc_max][NV] of this team
     double *max_g;        // [2][G] of this team
     double lambda0, ratio_thr, alpha;
-    int mode, n_iters, use_ratio, loss, G, s, trace_stride, nc_max, no_memo, sampling;
+    int mode, n_iters, use_ratio, loss, G, s, trace_stride, nc_max, no_memo, sampling, sobel_flags;
     unsigned epoch;       // exchanges done by this team in this launch
     int dead;             // a team exchange timed out: finish remaining problems as failed
     int stamps_on;        // debug phase stamps enabled
@@ -82,6 +82,7 @@ struct PC {
     int Hf, Wf, cs, cb, ce, ld, im_w, im_h, p0, M, c0, LC, G;
     UDiv dh, dw;
     int loss, no_memo, use_ratio, bilinear;
+    int sob_norm, sob_rep;  // FMPNP_LAYOUT_F: the in-gather Sobel's flags
     double alpha;
     double *part_g;       // this team's partial slots [2][nc_max][NV] (G > 1)
     int nc_max;
@@ -137,6 +138,8 @@ __device__ __forceinline__ PC load_pc() {
     q.bilinear = ufirst(c.sampling == FMPNP_BILINEAR ? 1 : 0);
     q.use_ratio = ufirst(c.use_ratio);
     q.alpha = ufirst(c.alpha);
+    q.sob_norm = ufirst(c.sobel_flags & 1);
+    q.sob_rep = ufirst((c.sobel_flags >> 1) & 1);
     q.part_g = ufirst(c.part_g);
     q.nc_max = ufirst(c.nc_max);
     q.stamps = ufirst(c.stamps_on) != 0;
@@ -741,12 +744,111 @@ __device__ __forceinline__ void gather_pipe(unsigned long long m, int off, bool 
 }
 
 // ---------------------------------------------------------------------------
+// FMPNP_LAYOUT_F: a dirty point's channel sums from the f plane alone.  The half-wave's
+// point reads its texel's 3x3 neighbourhood (zero outside the map, or clamped with
+// replicate padding) and forms gx, gy per channel in fp64 with the pack kernel's separable
+// expression (sx_j = (a_j + 2 d_j) + g_j, sy_j = g_j - a_j; gx = sx_+ - sx_-,
+// gy = (sy_- + 2 sy_0) + sy_+; a, d, g = rows above, at, below): exact for fp32 maps, i.e.
+// the reference's fp64 Sobel of the hypercolumn (helpers/utils.py:81-104) without the fp32
+// rounding the packed gradients carry.  Channel order and zero-filled second rounds as in
+// gather_half, so the sums do not depend on where the point sits.
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void sobel_acc(double a[8], const T *tap[9], int e, const T *pr, bool mask,
+                                          const bool ok[9], bool norm, bool zero) {
+    double v[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) v[k] = (zero || (mask && !ok[k])) ? 0.0 : (double)tap[k][e];
+    const double sxm = (v[0] + 2.0 * v[3]) + v[6], sym = v[6] - v[0];
+    const double sy0 = v[7] - v[1];
+    const double sxp = (v[2] + 2.0 * v[5]) + v[8], syp = v[8] - v[2];
+    double gx = sxp - sxm, gy = (sym + 2.0 * sy0) + syp;
+    if (norm) {
+        gx *= 0.125;
+        gy *= 0.125;
+    }
+    acc6(a, v[4], zero ? 0.0 : (double)pr[e], gx, gy);
+}
+
+// One point per trip, the whole wave on its channels (lane l: channels cb + l V + r 64 V):
+// the nine tap addresses and border masks are wave-uniform (scalar registers), ten 16-byte
+// loads per lane per round.
+template <typename T, bool MASK>
+__device__ __forceinline__ void gather_f_point(const T *__restrict__ feat, const int o[9], const bool ok[9],
+                                               const T *__restrict__ rf, int cs, int cb, int ce, int lane, bool vec,
+                                               bool norm, double a[8]) {
+    using VT = typename V16<T>::type;
+    constexpr int V = V16<T>::n;
+    if (vec) {
+        for (int c = cb + lane * V; c < ce; c += 64 * V) {
+            VT x[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) x[k] = gload<VT>(feat + (size_t)o[k] * cs + c);
+            const VT qv = gload<VT>(rf + c);
+            const T *t[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) t[k] = reinterpret_cast<const T *>(&x[k]);
+#pragma unroll
+            for (int e = 0; e < V; ++e) sobel_acc<T>(a, t, e, reinterpret_cast<const T *>(&qv), MASK, ok, norm, false);
+        }
+    } else {
+        for (int c = cb + lane * V; c < ce; c += 64 * V) {
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                const int ch = c + e;
+                const bool in = ch < ce;
+                const int chs = in ? ch : cb;
+                const T *tap[9];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) tap[k] = feat + (size_t)o[k] * cs + chs;
+                sobel_acc<T>(a, tap, 0, rf + chs, MASK, ok, norm, !in);
+            }
+        }
+    }
+}
+
+// Every dirty point of a block, one per trip; rc = (row << 16) | col of each lane's point.
+template <typename T>
+__device__ __forceinline__ void gather_f_block(unsigned long long m, int rc, bool hi, int lane, const T *feat,
+                                               const T *fref0, int cs, int cb, int ce, int ld, int Hf, int Wf,
+                                               bool vec, bool norm, bool rep, double *rec0, int e6, bool wlane) {
+    while (m) {
+        const int p = __builtin_ctzll(m);
+        m &= m - 1;
+        const int prc = __builtin_amdgcn_readlane(rc, p);
+        const int row = prc >> 16, col = prc & 0xffff;
+        int o[9];
+        bool ok[9];
+#pragma unroll
+        for (int dr = 0; dr < 3; ++dr)
+#pragma unroll
+            for (int dc = 0; dc < 3; ++dc) {
+                const int r = row + dr - 1, c = col + dc - 1;
+                const int rr = min(max(r, 0), Hf - 1), cc = min(max(c, 0), Wf - 1);
+                o[3 * dr + dc] = rr * Wf + cc;
+                ok[3 * dr + dc] = rep || (r == rr && c == cc);
+            }
+        const bool interior = rep || (row > 0 && row < Hf - 1 && col > 0 && col < Wf - 1);
+        double v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = 0.0;
+        const T *rf = fref0 + (size_t)p * ld;
+        if (interior) gather_f_point<T, false>(feat, o, ok, rf, cs, cb, ce, lane, vec, norm, v);
+        else gather_f_point<T, true>(feat, o, ok, rf, cs, cb, ce, lane, vec, norm, v);
+        double r = reduce8_in32(v, lane), r2 = r;
+        swap32(r, r2);  // the two halves hold the point's even / odd channel groups
+        r = r + r2;
+        if (wlane && !hi) rec0[(size_t)p * RECW + e6] = r;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // One evaluation at (Re, te) over the wave's blocks (no workgroup barrier inside).
 // Without the ratio test each block goes straight on to its chunk partials; with it the
 // loss values are parked in the records and the wave's max |rho| is returned.
 // PIPE: double-buffered gathers (latency variant: the VGPRs for two pairs in flight).
 // ---------------------------------------------------------------------------
-template <typename T, bool PIPE>
+template <typename T, bool PIPE, bool FL>
 __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ngath) {
     LMState &st = S();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l32 = lane & 31;
@@ -784,7 +886,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         // (exact products, a correctly rounded quotient of integers floors to the integer
         // quotient), computed here with invariant-multiplier division
         double Pc[3] = {0.0, 0.0, 1.0};
-        int off = -1;
+        int off = -1, rc = 0;
         Taps tp;
         if (valid) {
             transform_pt(Re, te, X[3 * i], X[3 * i + 1], X[3 * i + 2], Pc);
@@ -794,6 +896,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
                 const int row = (int)udiv((unsigned)y * (unsigned)q.Hf, q.dh);
                 const int col = (int)udiv((unsigned)x * (unsigned)q.Wf, q.dw);
                 off = row * q.Wf + col;
+                if (FL) rc = (row << 16) | col;
                 if (q.bilinear) bilinear_taps(qx, qy, q.Hf, q.Wf, q.im_w, q.im_h, tp);
             }
         }
@@ -808,7 +911,10 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         dbg_stamp(q.stamps, 0);
         const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
         const bool wlane = (lane & 3) == 0 && e6 < 6;
-        if (q.bilinear) {
+        if constexpr (FL) {
+            gather_f_block<T>(m, rc, hi, lane, feat, fref + (size_t)(p0 + blk * 64) * ld, cs, cb, ce, ld, q.Hf, q.Wf,
+                              vec, q.sob_norm != 0, q.sob_rep != 0, rec + (size_t)blk * 64 * RECW, e6, wlane);
+        } else if (q.bilinear) {
             gather_bil_block<T>(m, tp, hi, lane, feat, fref + (size_t)(p0 + blk * 64) * ld, cs, cb, ce, ld, vec,
                                 rec + (size_t)blk * 64 * RECW, e6, wlane);
         } else if (PIPE && onetrip) {
@@ -1231,6 +1337,7 @@ __global__ __launch_bounds__(NT, WPS) void lm_kernel(LaunchArgs a) {
         c.loss = a.opt.loss;
         c.no_memo = a.opt.no_memo;
         c.sampling = a.opt.sampling;
+        c.sobel_flags = a.opt.sobel_flags;
         c.stamps_on = a.stamps != nullptr;
         c.G = G;
         c.s = s;
@@ -1249,12 +1356,12 @@ __global__ __launch_bounds__(NT, WPS) void lm_kernel(LaunchArgs a) {
         PC q = load_pc();
         if constexpr (!TEAM) q.G = 1;
         q.use_ratio = RATIO ? 1 : 0;
-        if constexpr (VAR == VAR_GM) q.loss = FMPNP_GEMAN_MCCLURE;
+        if constexpr (VAR == VAR_GM || VAR == VAR_F_GM) q.loss = FMPNP_GEMAN_MCCLURE;
         q.bilinear = VAR == VAR_BILINEAR ? 1 : 0;
         long long ngath = 0;  // texel gathers of this wave for this problem
         while (!st.done) {
             // project, gather, loss (+ partials)
-            const double lmax = eval_pass<T, WPS == WPS_LATENCY>(q, mmax, ngath);
+            const double lmax = eval_pass<T, WPS == WPS_LATENCY, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST)>(q, mmax, ngath);
             if (q.use_ratio) {
                 if (!ratio_exchange(lmax)) break;
                 contrib_pass(q, mmax);

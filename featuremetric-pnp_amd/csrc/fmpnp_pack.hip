@@ -239,7 +239,7 @@ __device__ __forceinline__ void sb_put(Tout v, __amdgpu_buffer_rsrc_t rsrc, int 
 //   Tin = float : separable form, column sums then differences (6 fp64 ops per texel); exact
 //                 in fp64 for fp32 inputs, so the rounded result is the oracle's.
 //   Tin = double: the oracle's association (helpers/sobel_pytorch.py:9-59 order), bit-equal.
-template <typename Tin, typename Tout, bool FULL, bool NORM, bool NTS>
+template <typename Tin, typename Tout, bool FULL, bool NORM, bool NTS, bool GRAD>
 __device__ __forceinline__ void sb_row(const Tin *rm, const Tin *r0, const Tin *rp, __amdgpu_buffer_rsrc_t rsrc,
                                        int voff, int soff0, int tstride, int pstride, int ncols) {
     constexpr double sc = NORM ? 0.125 : 1.0;
@@ -258,8 +258,10 @@ __device__ __forceinline__ void sb_row(const Tin *rm, const Tin *r0, const Tin *
             if (FULL || k < ncols) {
                 const int so = soff0 + k * tstride;
                 sb_put<Tout, NTS>((Tout)f0, rsrc, voff, so);
-                sb_put<Tout, NTS>((Tout)(NORM ? gx * sc : gx), rsrc, voff, so + pstride);
-                sb_put<Tout, NTS>((Tout)(NORM ? gy * sc : gy), rsrc, voff, so + 2 * pstride);
+                if constexpr (GRAD) {
+                    sb_put<Tout, NTS>((Tout)(NORM ? gx * sc : gx), rsrc, voff, so + pstride);
+                    sb_put<Tout, NTS>((Tout)(NORM ? gy * sc : gy), rsrc, voff, so + 2 * pstride);
+                }
             }
             sxm = sx0; sym = sy0; sx0 = sxp; sy0 = syp; f0 = d2;
         }
@@ -274,8 +276,10 @@ __device__ __forceinline__ void sb_row(const Tin *rm, const Tin *r0, const Tin *
             if (FULL || k < ncols) {
                 const int so = soff0 + k * tstride;
                 sb_put<Tout, NTS>((Tout)d1, rsrc, voff, so);
-                sb_put<Tout, NTS>((Tout)(NORM ? gx * sc : gx), rsrc, voff, so + pstride);
-                sb_put<Tout, NTS>((Tout)(NORM ? gy * sc : gy), rsrc, voff, so + 2 * pstride);
+                if constexpr (GRAD) {
+                    sb_put<Tout, NTS>((Tout)(NORM ? gx * sc : gx), rsrc, voff, so + pstride);
+                    sb_put<Tout, NTS>((Tout)(NORM ? gy * sc : gy), rsrc, voff, so + 2 * pstride);
+                }
             }
             a0 = a1; a1 = a2; d0 = d1; d1 = d2; g0 = g1; g1 = g2;
         }
@@ -283,7 +287,7 @@ __device__ __forceinline__ void sb_row(const Tin *rm, const Tin *r0, const Tin *
 }
 
 // FAST: 16-B vector loads (aligned rows) and all 32 tile columns inside the map.
-template <typename Tin, typename Tout, bool NORM, bool NTS, bool FAST>
+template <typename Tin, typename Tout, bool NORM, bool NTS, bool FAST, bool GRAD>
 __device__ __forceinline__ void sobel_pack_body(const Tin *__restrict__ chw, int C, int H, int W, int cs, int rs,
                                                 int replicate, Tin *ring, __amdgpu_buffer_rsrc_t rsrc, int c0, int x0,
                                                 int y0, int dir) {
@@ -293,7 +297,7 @@ __device__ __forceinline__ void sobel_pack_body(const Tin *__restrict__ chw, int
     const int c = c0 + cc;
     const int wrun = __builtin_amdgcn_readfirstlane(run);  // wave-uniform: store offsets stay in SGPRs
     const int voff = (c < C ? c : 0) * (int)sizeof(Tout);
-    const int tstride = 3 * cs * (int)sizeof(Tout), pstride = cs * (int)sizeof(Tout);
+    const int tstride = (GRAD ? 3 : 1) * cs * (int)sizeof(Tout), pstride = cs * (int)sizeof(Tout);
     const int ncols = W - (x0 + wrun * SB_RUN);
 
     SbRow<Tin> r;
@@ -324,13 +328,13 @@ __device__ __forceinline__ void sobel_pack_body(const Tin *__restrict__ chw, int
             const Tin *r0 = ring + (y & 3) * SE + lo;
             const Tin *rp = ring + ((y + 1) & 3) * SE + lo;
             const int soff0 = ((y - y0) * W + x0 + wrun * SB_RUN) * tstride;
-            sb_row<Tin, Tout, FAST, NORM, NTS>(rm, r0, rp, rsrc, voff_s, soff0, tstride, pstride, ncols);
+            sb_row<Tin, Tout, FAST, NORM, NTS, GRAD>(rm, r0, rp, rsrc, voff_s, soff0, tstride, pstride, ncols);
         }
         if (more) sb_store<Tin>(r, ring + ((y + 2 * dir) & 3) * SE);
     }
 }
 
-template <typename Tin, typename Tout, bool NORM, bool NTS>
+template <typename Tin, typename Tout, bool NORM, bool NTS, bool GRAD>
 __global__ __launch_bounds__(SB_NT) void sobel_pack_kernel(const Tin *__restrict__ chw, int C, int H, int W,
                                                         Tout *__restrict__ out, int cs, int rs, int replicate,
                                                         int vec_ok, int ncb, int nxw, int ntiles, int xcd_map,
@@ -357,19 +361,19 @@ __global__ __launch_bounds__(SB_NT) void sobel_pack_kernel(const Tin *__restrict
     const int dir = (alt_dir && (yb & 1)) ? -1 : 1;
     const int y1 = min(y0 + rs, H);
     // descriptor over this tile's output rows [y0, y1) x all columns (byte offsets < 2^31)
-    const size_t texel_elems = (size_t)3 * cs;
+    const size_t texel_elems = (size_t)(GRAD ? 3 : 1) * cs;
     Tout *tile_base = out + (size_t)y0 * W * texel_elems;
     const unsigned tile_bytes = (unsigned)((size_t)(y1 - y0) * W * texel_elems * sizeof(Tout));
     __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_base, 0, tile_bytes, 0x00020000);
     if (vec_ok && x0 + SB_XW <= W)
-        sobel_pack_body<Tin, Tout, NORM, NTS, true>(chw, C, H, W, cs, rs, replicate, ring, rsrc, c0, x0, y0, dir);
+        sobel_pack_body<Tin, Tout, NORM, NTS, true, GRAD>(chw, C, H, W, cs, rs, replicate, ring, rsrc, c0, x0, y0, dir);
     else
-        sobel_pack_body<Tin, Tout, NORM, NTS, false>(chw, C, H, W, cs, rs, replicate, ring, rsrc, c0, x0, y0, dir);
+        sobel_pack_body<Tin, Tout, NORM, NTS, false, GRAD>(chw, C, H, W, cs, rs, replicate, ring, rsrc, c0, x0, y0, dir);
 }
 
 template <typename Tin, typename Tout>
 static hipError_t pack_t(const void *chw, const void *gx, const void *gy, int C, int H, int W, void *out, int cs,
-                         int normalized, int replicate, hipStream_t stream) {
+                         int normalized, int replicate, bool grad, hipStream_t stream) {
     if (gx) {
         dim3 grid((C + PK_CB - 1) / PK_CB, (W + PK_XW - 1) / PK_XW, (H + PK_RS - 1) / PK_RS);
         size_t lds = 3 * PK_CB * PK_LD * sizeof(Tin);
@@ -392,31 +396,35 @@ static hipError_t pack_t(const void *chw, const void *gx, const void *gy, int C,
     dim3 grid(xcd_map == 2 ? (nsp + 7) / 8 * 8 * ncb : xcd_map ? (ntiles + 7) / 8 * 8 : ntiles);
     size_t lds = (size_t)SB_SLOTS * SB_CB * SB_LD * sizeof(Tin);
     // the output descriptor of a workgroup spans its rs rows: byte offsets must stay below 2^31
-    if ((size_t)rs * W * 3 * cs * sizeof(Tout) >= ((size_t)1 << 31)) return hipErrorInvalidValue;
+    if ((size_t)rs * W * (grad ? 3 : 1) * cs * sizeof(Tout) >= ((size_t)1 << 31)) return hipErrorInvalidValue;
     // nt stores by default (the packed map is streamed out once; measured 2-17 % faster than
     // plain stores over cfg2..cfg5 shapes); FMPNP_PACK_NT=0 selects plain stores
     static const int nts = [] { const char *e = getenv("FMPNP_PACK_NT"); return !(e && *e == '0'); }();
-#define SB_LAUNCH(NORM, NTS)                                                                                    \
-    hipLaunchKernelGGL((sobel_pack_kernel<Tin, Tout, NORM, NTS>), grid, dim3(SB_NT), lds, stream,              \
+#define SB_LAUNCH(NORM, NTS, GRAD)                                                                              \
+    hipLaunchKernelGGL((sobel_pack_kernel<Tin, Tout, NORM, NTS, GRAD>), grid, dim3(SB_NT), lds, stream,        \
                        (const Tin *)chw, C, H, W, (Tout *)out, cs, rs, replicate, vec_ok, ncb, nxw, ntiles, xcd_map, alt_dir)
-    if (normalized) {
-        if (nts) SB_LAUNCH(true, true); else SB_LAUNCH(true, false);
+    if (!grad) {  // FMPNP_LAYOUT_F: the channels-last f plane only (the LM kernel forms the gradients)
+        if (nts) SB_LAUNCH(false, true, false); else SB_LAUNCH(false, false, false);
+    } else if (normalized) {
+        if (nts) SB_LAUNCH(true, true, true); else SB_LAUNCH(true, false, true);
     } else {
-        if (nts) SB_LAUNCH(false, true); else SB_LAUNCH(false, false);
+        if (nts) SB_LAUNCH(false, true, true); else SB_LAUNCH(false, false, true);
     }
 #undef SB_LAUNCH
     return hipGetLastError();
 }
 
 hipError_t launch_pack(const void *chw, const void *gx, const void *gy, int dtype_in, int C, int H, int W, void *out,
-                       int dtype_out, int cs, int normalized, int replicate, hipStream_t stream) {
+                       int dtype_out, int cs, int normalized, int replicate, hipStream_t stream, int planes) {
+    const bool grad = planes != 1;
+    if (!grad && gx) return hipErrorInvalidValue;
     if (dtype_in == FMPNP_F32 && dtype_out == FMPNP_F32)
-        return pack_t<float, float>(chw, gx, gy, C, H, W, out, cs, normalized, replicate, stream);
+        return pack_t<float, float>(chw, gx, gy, C, H, W, out, cs, normalized, replicate, grad, stream);
     if (dtype_in == FMPNP_F32 && dtype_out == FMPNP_F64)
-        return pack_t<float, double>(chw, gx, gy, C, H, W, out, cs, normalized, replicate, stream);
+        return pack_t<float, double>(chw, gx, gy, C, H, W, out, cs, normalized, replicate, grad, stream);
     if (dtype_in == FMPNP_F64 && dtype_out == FMPNP_F32)
-        return pack_t<double, float>(chw, gx, gy, C, H, W, out, cs, normalized, replicate, stream);
-    return pack_t<double, double>(chw, gx, gy, C, H, W, out, cs, normalized, replicate, stream);
+        return pack_t<double, float>(chw, gx, gy, C, H, W, out, cs, normalized, replicate, grad, stream);
+    return pack_t<double, double>(chw, gx, gy, C, H, W, out, cs, normalized, replicate, grad, stream);
 }
 
 // fref gather (optimize_feature_pnp.py:51-56): relative_shape = [H_ref/img0, W_ref/img1];

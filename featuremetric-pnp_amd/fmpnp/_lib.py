@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libfmpnp.so")
 # enums / constants (include/fmpnp.h)
 SQUARED, HUBER, CAUCHY, GEMAN_MCCLURE, BARRON = 0, 1, 2, 3, 4
 NEAREST, BILINEAR = 0, 1
+LAYOUT_FGRAD, LAYOUT_F = 0, 1
 F32, F64 = 0, 1
 MODE_FORWARD, MODE_COMPUTE_COST = 0, 1
 STATUS_OK, STATUS_NO_SUPPORT, STATUS_NAN, STATUS_NO_SUPPORT_TRIAL, STATUS_SYNC_TIMEOUT = 0, 1, 2, 4, 8
@@ -26,7 +27,8 @@ class Options(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int), ("n_iters", ctypes.c_int), ("lambda0", ctypes.c_double),
                 ("use_ratio", ctypes.c_int), ("ratio_threshold", ctypes.c_double), ("loss", ctypes.c_int),
                 ("barron_alpha", ctypes.c_double), ("sampling", ctypes.c_int), ("dtype", ctypes.c_int),
-                ("wgs_per_problem", ctypes.c_int), ("max_teams", ctypes.c_int), ("no_memo", ctypes.c_int)]
+                ("wgs_per_problem", ctypes.c_int), ("max_teams", ctypes.c_int), ("no_memo", ctypes.c_int),
+                ("layout", ctypes.c_int), ("sobel_flags", ctypes.c_int)]
 
 
 class Problem(ctypes.Structure):
@@ -52,7 +54,7 @@ class TraceEntry(ctypes.Structure):
 
 
 EXPORTS = ["fmpnp_abi_version", "fmpnp_build_info", "fmpnp_device_check", "fmpnp_pack_features",
-           "fmpnp_gather_reference", "fmpnp_gather_reference_async", "fmpnp_pack_features_batch",
+           "fmpnp_gather_reference", "fmpnp_gather_reference_async", "fmpnp_pack_features_batch", "fmpnp_pack_features_f",
            "fmpnp_gather_reference_batch", "fmpnp_workspace_size", "fmpnp_refine_batch_async", "fmpnp_refine_batch",
            "fmpnp_last_launch", "fmpnp_debug_stamps"]
 
@@ -83,7 +85,9 @@ def load():
     L.fmpnp_gather_reference.restype = i
     L.fmpnp_gather_reference_async.argtypes = [vp, i, i, i, i, vp, i, i, i, vp, i, i, vp, vp]
     L.fmpnp_gather_reference_async.restype = i
-    L.fmpnp_pack_features_batch.argtypes = [i, vp, vp, vp, i, i, i, i, vp]
+    L.fmpnp_pack_features_batch.argtypes = [i, vp, vp, vp, i, i, i, i, i, vp]
+    L.fmpnp_pack_features_f.argtypes = [vp, i, i, i, i, vp, i, i, vp]
+    L.fmpnp_pack_features_f.restype = i
     L.fmpnp_pack_features_batch.restype = i
     L.fmpnp_gather_reference_batch.argtypes = [i, vp, vp, vp, vp, i, i, vp, vp, i, i, vp, vp]
     L.fmpnp_gather_reference_batch.restype = i

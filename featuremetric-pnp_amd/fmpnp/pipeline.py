@@ -43,7 +43,7 @@ def _streams(device):
 
 class RefinePipeline:
     def __init__(self, image_shape=None, storage=torch.float32, device=None, depth=2, model_kwargs=None,
-                 sampling="nearest"):
+                 sampling="nearest", layout=None):
         cfg = config.adapter_kwargs()
         self.image_shape = tuple(image_shape or cfg.get("image_shape", (1024, 1024)))
         self.storage = storage
@@ -55,6 +55,12 @@ class RefinePipeline:
         self.options = _rf.make_options(kw["n_iters"], kw["lambda_"], loss_code, alpha, kw.get("ratio_threshold"),
                                         _rf._dtype_code(storage), sampling=sampling)
         self.depth = max(1, int(depth))
+        # "f" (f plane only, gradients formed in the LM gather) wherever it applies: fp32
+        # texels, nearest sampling; "fgrad" (the packed f, gx, gy planes) otherwise
+        f_ok = storage == torch.float32 and sampling == "nearest"
+        self.layout = layout or ("f" if f_ok else "fgrad")
+        if self.layout == "f" and not f_ok:
+            raise ValueError("layout 'f' needs fp32 storage and nearest sampling")
         self.prep, self.solve = _streams(self.device)
         self.slabs = [None] * self.depth        # flat uint8 device buffers holding a batch's packed maps
         self.slab_free = [None] * self.depth    # event: the last launch that read the slab finished
@@ -80,7 +86,8 @@ class RefinePipeline:
         q_dt = qmaps[0].dtype if qmaps and qmaps[0].dtype in (torch.float32, torch.float64) else torch.float32
         r_dt = rmaps[0].dtype if rmaps and rmaps[0].dtype in (torch.float32, torch.float64) else torch.float32
         es = torch.empty(0, dtype=storage).element_size()
-        shapes = [(m.shape[1], m.shape[2], 3, _rf._round4(m.shape[0])) for m in qmaps]
+        planes = 3 if self.layout == "fgrad" else 1
+        shapes = [(m.shape[1], m.shape[2], planes, _rf._round4(m.shape[0])) for m in qmaps]
         sizes = [int(np.prod(sh)) * es for sh in shapes]
         starts = np.concatenate([[0], np.cumsum([(b + _ALIGN - 1) // _ALIGN * _ALIGN for b in sizes])]).astype(int)
         inl = [np.asarray(p.reference_inliers, np.float64).reshape(-1, 2) for (_, _, p, _) in queries]
@@ -91,7 +98,10 @@ class RefinePipeline:
             qmaps = [_rf._as_device(m, dev, q_dt) for m in qmaps]   # no-ops for device maps of the batch dtype
             rmaps = [_rf._as_device(m, dev, r_dt) for m in rmaps]
             slab = self._slab(k, max(int(starts[-1]), 1))
-            outs = [slab[starts[i]:starts[i] + sizes[i]].view(storage).view(shapes[i]) for i in range(nq)]
+            outs = [slab[starts[i]:starts[i] + sizes[i]].view(storage).view(shapes[i] if planes == 3 else
+                                                                              (shapes[i][0], shapes[i][1],
+                                                                               shapes[i][3]))
+                    for i in range(nq)]
             for i in range(nq):
                 if shapes[i][3] != qmaps[i].shape[0]:
                     outs[i].zero_()  # padding channels stay zero (the kernel writes c < C only)
@@ -113,7 +123,8 @@ class RefinePipeline:
                                                     (qmaps[i].shape[0], shapes[i][0], shapes[i][1], shapes[i][3])])
             rc = L.fmpnp_pack_features_batch(
                 nq, (vp * nq)(*[m.data_ptr() for m in qmaps]), (vp * nq)(*[o.data_ptr() for o in outs]), shape_arr,
-                _rf._dtype_code(q_dt), _rf._dtype_code(storage), 0, 0, s)                    # :57, :61
+                _rf._dtype_code(q_dt), _rf._dtype_code(storage), 0, 0,
+                _lib.LAYOUT_F if self.layout == "f" else _lib.LAYOUT_FGRAD, s)                # :57, :61
             _lib.check(rc, "fmpnp_pack_features_batch")
             rshape = (ctypes.c_int * (3 * nq))(*[v for m in rmaps for v in m.shape])
             base = dflat.data_ptr()
@@ -125,7 +136,8 @@ class RefinePipeline:
                 vp(err.data_ptr()), s)                                                        # :51-56
             _lib.check(rc, "fmpnp_gather_reference_batch")
             for i, (_, _, pred, K) in enumerate(queries):
-                feats = _rf.PackedFeatures(outs[i], qmaps[i].shape[0], shapes[i][0], shapes[i][1], shapes[i][3])
+                feats = _rf.PackedFeatures(outs[i], qmaps[i].shape[0], shapes[i][0], shapes[i][1], shapes[i][3],
+                                           self.layout, 0)
                 T = np.asarray(pred.matrix, dtype=np.float64)
                 probs.append(_rf.make_problem(feats, frefs[i], dflat[offs[nq + i]:offs[nq + i + 1]].view(-1, 3),
                                               np.asarray(K, np.float64).reshape(3, 3), self.image_shape[0],

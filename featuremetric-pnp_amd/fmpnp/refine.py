@@ -29,12 +29,16 @@ def _round4(c):
 
 @dataclass
 class PackedFeatures:
-    """Channels-last feature texels on the device: buf[H][W][3][cstride] = (f, gx, gy)."""
+    """Channels-last feature texels on the device: buf[H][W][3][cstride] = (f, gx, gy)
+    (layout "fgrad"), or buf[H][W][cstride] = f only (layout "f": the LM kernel forms the
+    Sobel gradients with `sobel_flags` when it gathers a texel)."""
     buf: torch.Tensor
     C: int
     H: int
     W: int
     cstride: int
+    layout: str = "fgrad"
+    sobel_flags: int = 0
 
     @property
     def dtype(self):
@@ -59,11 +63,15 @@ def _as_device(x, device, dtype=None, non_blocking=False):
 
 
 def pack_features(fmap, gx=None, gy=None, storage=None, device=None, sobel_normalized=False,
-                  sobel_replicate_pad=False, stream=None, out=None):
+                  sobel_replicate_pad=False, stream=None, out=None, layout="fgrad"):
     """[C,H,W] (or [1,C,H,W]) feature map -> PackedFeatures.
 
-    out: optional caller-owned contiguous device tensor [H, W, 3, cstride] of the
-    storage dtype to pack into (cstride = C rounded up to 4; a padded one is zeroed first).
+    layout="f": the channels-last f plane only (a third of the bytes); the Sobel flags are
+    recorded for the LM kernel, which computes the gradients itself (fp32 storage only).
+
+    out: optional caller-owned contiguous device tensor [H, W, 3, cstride] ([H, W, cstride]
+    for layout "f") of the storage dtype to pack into (cstride = C rounded up to 4; a padded
+    one is zeroed first).
 
     Without gx/gy the Sobel gradients are computed on the device (fused kernel;
     vendored kornia Sobel by default: unnormalised, zero padded,
@@ -82,6 +90,11 @@ def pack_features(fmap, gx=None, gy=None, storage=None, device=None, sobel_norma
     storage = storage or in_dt
     C, H, W = fmap.shape
     cs = _round4(C)
+    if layout not in ("fgrad", "f"):
+        raise ValueError("layout must be 'fgrad' or 'f'")
+    if layout == "f" and (gx is not None or storage != torch.float32):
+        raise ValueError("layout 'f' packs fp32 f only (the gradients are formed by the LM kernel)")
+    oshape = (H, W, 3, cs) if layout == "fgrad" else (H, W, cs)
     with torch.cuda.device(device):
         f = _as_device(fmap, device, in_dt)
         gxd = gyd = None
@@ -91,26 +104,31 @@ def pack_features(fmap, gx=None, gy=None, storage=None, device=None, sobel_norma
             gyd = _as_device(gy.reshape(C, H, W) if isinstance(gy, torch.Tensor) else np.asarray(gy).reshape(C, H, W),
                              device, in_dt)
         if out is not None:
-            if (tuple(out.shape) != (H, W, 3, cs) or out.dtype != storage or out.device != device
+            if (tuple(out.shape) != oshape or out.dtype != storage or out.device != device
                     or not out.is_contiguous()):
-                raise ValueError(f"out must be a contiguous {storage} tensor [{H}, {W}, 3, {cs}] on {device}")
+                raise ValueError(f"out must be a contiguous {storage} tensor {list(oshape)} on {device}")
             if cs != C:
                 out.zero_()
         elif cs != C:
-            out = torch.zeros((H, W, 3, cs), dtype=storage, device=device)
+            out = torch.zeros(oshape, dtype=storage, device=device)
         else:
-            out = torch.empty((H, W, 3, cs), dtype=storage, device=device)
+            out = torch.empty(oshape, dtype=storage, device=device)
         s = stream if stream is not None else _lib.stream_ptr(device)
-        rc = _lib.load().fmpnp_pack_features(
-            ctypes.c_void_p(f.data_ptr()), ctypes.c_void_p(gxd.data_ptr()) if gxd is not None else None,
-            ctypes.c_void_p(gyd.data_ptr()) if gyd is not None else None, _dtype_code(in_dt), C, H, W,
-            ctypes.c_void_p(out.data_ptr()), _dtype_code(storage), cs, int(bool(sobel_normalized)),
-            int(bool(sobel_replicate_pad)), s)
+        if layout == "f":
+            rc = _lib.load().fmpnp_pack_features_f(ctypes.c_void_p(f.data_ptr()), _dtype_code(in_dt), C, H, W,
+                                                   ctypes.c_void_p(out.data_ptr()), _dtype_code(storage), cs, s)
+        else:
+            rc = _lib.load().fmpnp_pack_features(
+                ctypes.c_void_p(f.data_ptr()), ctypes.c_void_p(gxd.data_ptr()) if gxd is not None else None,
+                ctypes.c_void_p(gyd.data_ptr()) if gyd is not None else None, _dtype_code(in_dt), C, H, W,
+                ctypes.c_void_p(out.data_ptr()), _dtype_code(storage), cs, int(bool(sobel_normalized)),
+                int(bool(sobel_replicate_pad)), s)
         _lib.check(rc, "fmpnp_pack_features")
         # keep inputs alive until the kernel has consumed them
         if f.data_ptr() != fmap.data_ptr() or gxd is not None:
             torch.cuda.current_stream(device).synchronize()
-    return PackedFeatures(out, C, H, W, cs)
+    flags = int(bool(sobel_normalized)) | (int(bool(sobel_replicate_pad)) << 1)
+    return PackedFeatures(out, C, H, W, cs, layout, flags if layout == "f" else 0)
 
 
 def pad_reference(fref, cstride, storage, device):
@@ -221,6 +239,20 @@ def make_problem(feats, fref, pts3d, K, im_width, im_height, R0, t0, c_begin=0, 
 _SAMPLING = {"nearest": _lib.NEAREST, "bilinear": _lib.BILINEAR}
 
 
+def bind_layout(problems, options):
+    """The options with `layout` / `sobel_flags` taken from the problems' packed features
+    (every problem of a launch shares one layout)."""
+    lays = {(p.feats.layout, p.feats.sobel_flags) for p in problems}
+    if len(lays) > 1:
+        raise ValueError("all problems of a launch must share one feature layout")
+    o = _lib.Options.from_buffer_copy(options)
+    if lays:
+        lay, flags = lays.pop()
+        o.layout = _lib.LAYOUT_F if lay == "f" else _lib.LAYOUT_FGRAD
+        o.sobel_flags = flags
+    return o
+
+
 def make_options(n_iters, lambda0=0.01, loss=_lib.SQUARED, barron_alpha=0.0, ratio_threshold=None,
                  dtype=_lib.F32, mode=_lib.MODE_FORWARD, wgs_per_problem=0, max_teams=0, memoize=True,
                  sampling="nearest"):
@@ -273,6 +305,7 @@ def refine(problems, options, trace=False):
     descs = (_lib.Problem * n)(*[p.descriptor() for p in problems])
     if descs[0].feat and options.dtype != problems[0].feats.dtype_code:
         raise TypeError("options.dtype does not match the packed features")
+    options = bind_layout(problems, options)
     res = (_lib.Result * n)()
     stride = max(1, options.n_iters + 1) if trace else 0
     tr = (_lib.TraceEntry * (n * stride))() if trace else None
@@ -295,7 +328,7 @@ class AsyncBatch:
 
     def __init__(self, problems, options, non_blocking=False):
         self.problems = list(problems)
-        self.options = options
+        self.options = bind_layout(self.problems, options)
         n = len(self.problems)
         self.n = n
         self.dev = self.problems[0].feats.buf.device
@@ -307,7 +340,7 @@ class AsyncBatch:
                                 dtype=torch.uint8)
         self.d_descs.copy_(host.pin_memory() if non_blocking else host, non_blocking=non_blocking)
         self.d_res = torch.zeros(ctypes.sizeof(_lib.Result) * n, dtype=torch.uint8, device=self.dev)
-        ws = _lib.load().fmpnp_workspace_size(self.descs_host, n, ctypes.byref(options))
+        ws = _lib.load().fmpnp_workspace_size(self.descs_host, n, ctypes.byref(self.options))
         if ws == 0:
             raise _lib.FmpnpError("fmpnp_workspace_size failed (invalid problems/options)")
         self.d_ws = torch.empty(ws, dtype=torch.uint8, device=self.dev)

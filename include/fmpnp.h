@@ -12,7 +12,7 @@
  *          indexing_ / points_within_image      featurePnP/model.py:74-117,
  *          ratio_threshold_feature_errors       featurePnP/model.py:120-129,
  *          so3exp_map                           featurePnP/helpers/utils.py:209-221.
- *   fmpnp_pack_features / fmpnp_pack_features_batch
+ *   fmpnp_pack_features / fmpnp_pack_features_batch / fmpnp_pack_features_f
  *       replaces sobel_filter + the fp64 cast   featurePnP/helpers/utils.py:81-104,
  *                                               optimize_feature_pnp.py:57,61
  *       (fused Sobel + channels-last [H][W][3][C] packing).
@@ -56,6 +56,13 @@ typedef enum {
 typedef enum { FMPNP_F32 = 0, FMPNP_F64 = 1 } fmpnp_dtype;
 
 typedef enum {
+    FMPNP_LAYOUT_FGRAD = 0, /* feat = [Hf][Wf][3][cstride]: f, gx, gy (fmpnp_pack_features) */
+    FMPNP_LAYOUT_F = 1      /* feat = [Hf][Wf][cstride]: f only (fmpnp_pack_features_f); the LM kernel
+                               forms a texel's Sobel gradients from its 3x3 neighbourhood, in fp64,
+                               when it gathers the texel.  fp32 storage, nearest sampling. */
+} fmpnp_layout;
+
+typedef enum {
     FMPNP_MODE_FORWARD = 0,       /* sparseFeaturePnP.forward */
     FMPNP_MODE_COMPUTE_COST = 1   /* sparseFeaturePnP.compute_cost at (R0, t0) */
 } fmpnp_mode;
@@ -89,10 +96,14 @@ typedef struct {
     int no_memo;            /* 1: re-gather every point's texel at every evaluation (the
                                reference's data movement); 0 (default): re-gather only points
                                whose texel changed -- bit-identical results */
+    int layout;             /* fmpnp_layout of every problem's feat */
+    int sobel_flags;        /* FMPNP_LAYOUT_F: bit 0 normalized (/8), bit 1 replicate padding
+                               (the flags fmpnp_pack_features would have been given) */
 } fmpnp_options;
 
 typedef struct {
-    const void *feat;       /* device, [Hf][Wf][3][cstride] of dtype: planes f, gx, gy */
+    const void *feat;       /* device, [Hf][Wf][3][cstride] of dtype: planes f, gx, gy
+                               (FMPNP_LAYOUT_F: [Hf][Wf][cstride], f only) */
     const void *fref;       /* device, [N][ld_ref] of dtype; columns [c_begin, c_end) used */
     const double *pts3d;    /* device, [N][3] fp64 */
     int Hf, Wf, cstride, c_begin, c_end, ld_ref, N;
@@ -136,6 +147,11 @@ int fmpnp_pack_features(const void *chw, const void *gx_chw, const void *gy_chw,
                         int W, void *out, int dtype_out, int cstride, int sobel_normalized,
                         int sobel_replicate_pad, void *hip_stream);
 
+/* Channels-last copy of f only, [H][W][cstride] (dtype_out): the FMPNP_LAYOUT_F input of
+ * the LM kernel, a third of fmpnp_pack_features' output bytes. */
+int fmpnp_pack_features_f(const void *chw, int dtype_in, int C, int H, int W, void *out, int dtype_out,
+                          int cstride, void *hip_stream);
+
 /* fref gather of optimize_feature_pnp.py:51-56: for each of the N reference
  * inliers (x, y) (device [N][2] fp64), row = trunc(y * W_ref / img1),
  * col = trunc(x * H_ref / img0) of ref_chw [C][H_ref][W_ref] -> out [N][ld_out]. */
@@ -158,7 +174,8 @@ int fmpnp_gather_reference_async(const void *ref_chw, int dtype_in, int C, int H
  * reference map i; err_flags is a DEVICE int[n] the caller zeroes (set as in
  * fmpnp_gather_reference_async).  Every item is validated before anything is launched. */
 int fmpnp_pack_features_batch(int n, const void *const *chw, void *const *out, const int *shape, int dtype_in,
-                              int dtype_out, int sobel_normalized, int sobel_replicate_pad, void *hip_stream);
+                              int dtype_out, int sobel_normalized, int sobel_replicate_pad, int layout,
+                              void *hip_stream);
 int fmpnp_gather_reference_batch(int n, const void *const *ref_chw, const int *ref_shape,
                                  const double *const *ref_inliers, const int *n_inliers, int img0, int img1,
                                  void *const *out, const int *ld_out, int dtype_in, int dtype_out, int *err_flags,

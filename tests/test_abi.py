@@ -77,12 +77,24 @@ def test_entry_points_reject_bad_arguments_without_a_device():
     # batched forms: negative counts, missing arrays, and one bad item among good ones are
     # refused before anything is launched
     vp = ctypes.c_void_p
-    assert L.fmpnp_pack_features_batch(-1, None, None, None, 0, 0, 0, 0, None) == -1
-    assert L.fmpnp_pack_features_batch(1, None, None, None, 0, 0, 0, 0, None) == -1
-    assert L.fmpnp_pack_features_batch(0, None, None, None, 0, 0, 0, 0, None) == 0
+    assert L.fmpnp_pack_features_batch(-1, None, None, None, 0, 0, 0, 0, 0, None) == -1
+    assert L.fmpnp_pack_features_batch(1, None, None, None, 0, 0, 0, 0, 0, None) == -1
+    assert L.fmpnp_pack_features_batch(0, None, None, None, 0, 0, 0, 0, 0, None) == 0
     two = (vp * 2)(1, 2)
     shape = (ctypes.c_int * 8)(4, 2, 2, 4, 4, 2, 2, 3)  # item 1: cstride < C
-    assert L.fmpnp_pack_features_batch(2, two, two, shape, 0, 0, 0, 0, None) == -1
+    assert L.fmpnp_pack_features_batch(2, two, two, shape, 0, 0, 0, 0, 0, None) == -1
+    assert L.fmpnp_pack_features_batch(0, None, None, None, 0, 0, 0, 0, 7, None) == -1  # unknown layout
+    assert L.fmpnp_pack_features_f(None, 0, 1, 1, 1, None, 0, 1, None) == -1
+    # the f-only layout is fp32 with nearest sampling
+    # (option checks run before any problem or device access)
+    pb, res = _lib.Problem(), _lib.Result()
+    o = _lib.Options()
+    o.layout, o.dtype = _lib.LAYOUT_F, _lib.F64
+    assert L.fmpnp_refine_batch(ctypes.byref(pb), 1, ctypes.byref(o), ctypes.byref(res), None, 0, None) == -1
+    o.dtype, o.sampling = _lib.F32, _lib.BILINEAR
+    assert L.fmpnp_refine_batch(ctypes.byref(pb), 1, ctypes.byref(o), ctypes.byref(res), None, 0, None) == -1
+    o.sampling, o.layout = _lib.NEAREST, 5
+    assert L.fmpnp_refine_batch(ctypes.byref(pb), 1, ctypes.byref(o), ctypes.byref(res), None, 0, None) == -1
     assert L.fmpnp_gather_reference_batch(1, None, None, None, None, 1, 1, None, None, 0, 0, None, None) == -1
     rshape = (ctypes.c_int * 6)(4, 2, 2, 4, 2, 2)
     n_in = (ctypes.c_int * 2)(3, -1)                    # item 1: negative point count

@@ -24,7 +24,7 @@ def test_batched_pack_and_gather_equal_single_calls():
     shape_arr = (ctypes.c_int * 12)(*[v for (C, H, W), b in zip(shapes, single) for v in (C, H, W, b.shape[3])])
     rc = L.fmpnp_pack_features_batch(3, (vp * 3)(*[m.data_ptr() for m in maps]),
                                      (vp * 3)(*[o.data_ptr() for o in outs]), shape_arr, _lib.F32, _lib.F32, 0, 0,
-                                     _lib.stream_ptr(dev))
+                                     _lib.LAYOUT_FGRAD, _lib.stream_ptr(dev))
     _lib.check(rc, "pack batch")
     torch.cuda.synchronize()
     for a, b in zip(single, outs):
