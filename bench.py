@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--no-nomemo", action="store_true", help="skip the memoisation-off comparison launch")
     ap.add_argument("--no-bilinear", action="store_true", help="skip the bilinear-sampling launch")
     ap.add_argument("--no-pipeline", action="store_true", help="skip the end-to-end (pack + gather + LM) leg")
+    ap.add_argument("--no-layout-f", action="store_true", help="skip the f-only layout launch")
     return ap.parse_args()
 
 
@@ -168,6 +169,38 @@ def main():
               "frac": round(nm_bytes / nm_s / HBM_PEAK, 4), "poses_bit_identical_to_memoised": bool(same)}
         del batch_nm
 
+    # FMPNP_LAYOUT_F: the same queries with only the f plane in HBM (the LM gather forms the
+    # Sobel gradients), plus that layout's pack kernel (a channels-last copy)
+    lf = {}
+    if not args.no_layout_f:
+        keep_f = []
+        for q in range(B):
+            inp = synth.problem_inputs(N_PTS, C, HF, WF, seed=rank * 100003 + q, device=dev)
+            feats = rf.pack_features(inp["fmap"], storage=torch.float32, device=dev, layout="f")
+            keep_f.append(rf.make_problem(feats, inp["fref"], inp["pts3d"], inp["K"], inp["im_width"],
+                                          inp["im_height"], inp["R0"], inp["t0"]))
+            del inp
+        batch_f = rf.AsyncBatch(keep_f, opts)
+        batch_f.launch()
+        torch.cuda.synchronize()
+        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = max(1, min(args.steps, 5))
+        s_ev.record(stream)
+        for _ in range(reps):
+            batch_f.launch()
+        e_ev.record(stream)
+        torch.cuda.synchronize()
+        f_s = s_ev.elapsed_time(e_ev) / reps / 1e3
+        res_f = batch_f.results()
+        f_gath = int(sum(r["texel_gathers"] for r in res_f))
+        lf = {"ms_per_launch": round(f_s * 1e3, 4), "pose_refinements_per_s": round(B / f_s, 1),
+              "gathered_bytes_per_launch": f_gath * 40 * C + B * N_PTS * 24,
+              "bytes_rule": "per texel gather 9 neighbours x 4C (f) + 4C fref; fp64 point",
+              "max_rot_diff_vs_fgrad_rad": float(max(np.arccos(np.clip((np.trace(a["R"].T @ b["R"]) - 1) / 2, -1, 1))
+                                                     for a, b in zip(res, res_f))),
+              "statuses": sorted({r["status"] for r in res_f})}
+        del batch_f, keep_f
+
     # bilinear sampling (extension, FMPNP_BILINEAR): every supported point reads its 2x2 taps
     # of f, gx, gy plus fref at every evaluation -- SURVEY.md 8d's N*(52C+24) bytes per GN
     # iteration, no memoisation: the bandwidth-bound form of the loop
@@ -241,6 +274,7 @@ def main():
                                  "HBM-bound form"},
             "no_memo": nm,
             "bilinear": bil,
+            "layout_f": lf,
             "statuses": statuses,
         }
         out.update(extras)
@@ -310,6 +344,27 @@ def run_extras(args, dev, probs, keep, opts, rf, _lib, synth):
     out["pack"] = {"ms": round(pms, 4), "GB_per_s": round(pbytes / (pms / 1e3) / 1e9, 1),
                    "frac_of_peak": round(pbytes / (pms / 1e3) / HBM_PEAK, 4),
                    "bytes_rule": "16C per texel (4C read + 12C written), %d distinct maps rotated" % NP}
+    # the f-only layout's pack (FMPNP_LAYOUT_F): a channels-last copy, 4C read + 4C written
+    outs_f = [torch.empty((HF, WF, C), dtype=torch.float32, device=dev) for _ in range(NP)]
+
+    def pack_f(i):
+        rc = L.fmpnp_pack_features_f(ctypes.c_void_p(fms[i % NP].data_ptr()), _lib.F32, C, HF, WF,
+                                     ctypes.c_void_p(outs_f[i % NP].data_ptr()), _lib.F32, C, st)
+        _lib.check(rc, "pack_f")
+    for i in range(NP):
+        pack_f(i)
+    torch.cuda.synchronize()
+    s.record(torch.cuda.current_stream(dev))
+    for i in range(reps):
+        pack_f(i)
+    e.record(torch.cuda.current_stream(dev))
+    torch.cuda.synchronize()
+    fms_ = s.elapsed_time(e) / reps
+    fbytes = 8 * C * HF * WF
+    out["pack_f"] = {"ms": round(fms_, 4), "GB_per_s": round(fbytes / (fms_ / 1e3) / 1e9, 1),
+                     "frac_of_peak": round(fbytes / (fms_ / 1e3) / HBM_PEAK, 4),
+                     "bytes_rule": "8C per texel (4C read + 4C written), %d distinct maps rotated" % NP}
+    del outs_f
     del fms, outs
     # end to end from CHW hypercolumns (fmpnp.pipeline.RefinePipeline): pack + reference
     # gather + LM per batch, preparation of batch i+1 on a second stream under batch i's LM

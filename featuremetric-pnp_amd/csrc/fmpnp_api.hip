@@ -223,9 +223,9 @@ int fmpnp_gather_reference(const void *ref_chw, int dtype_in, int C, int H_ref, 
 
 int fmpnp_pack_features_f(const void *chw, int dtype_in, int C, int H, int W, void *out, int dtype_out,
                           int cstride, void *hip_stream) {
-    if (!chw || !out || C <= 0 || H <= 0 || W <= 0 || cstride < C) return FMPNP_EINVAL;
-    if ((dtype_in != FMPNP_F32 && dtype_in != FMPNP_F64) || (dtype_out != FMPNP_F32 && dtype_out != FMPNP_F64))
-        return FMPNP_EINVAL;
+    if (!chw || !out || C <= 0 || H <= 0 || W <= 0 || cstride < C || cstride % 4) return FMPNP_EINVAL;
+    if ((dtype_in != FMPNP_F32 && dtype_in != FMPNP_F64) || dtype_out != FMPNP_F32) return FMPNP_EINVAL;
+    if ((uintptr_t)out % 16) return FMPNP_EALIGN;
     return (int)launch_pack(chw, nullptr, nullptr, dtype_in, C, H, W, out, dtype_out, cstride, 0, 0,
                             (hipStream_t)hip_stream, 1);
 }
@@ -237,9 +237,11 @@ int fmpnp_pack_features_batch(int n, const void *const *chw, void *const *out, c
     if (layout != FMPNP_LAYOUT_FGRAD && layout != FMPNP_LAYOUT_F) return FMPNP_EINVAL;
     if ((dtype_in != FMPNP_F32 && dtype_in != FMPNP_F64) || (dtype_out != FMPNP_F32 && dtype_out != FMPNP_F64))
         return FMPNP_EINVAL;
+    if (layout == FMPNP_LAYOUT_F && dtype_out != FMPNP_F32) return FMPNP_EINVAL;
     for (int i = 0; i < n; ++i) {  // every item checked before anything is launched
         const int *sh = shape + 4 * i;
         if (!chw[i] || !out[i] || sh[0] <= 0 || sh[1] <= 0 || sh[2] <= 0 || sh[3] < sh[0]) return FMPNP_EINVAL;
+        if (layout == FMPNP_LAYOUT_F && (sh[3] % 4 || (uintptr_t)out[i] % 16)) return FMPNP_EINVAL;
     }
     for (int i = 0; i < n; ++i) {
         const int *sh = shape + 4 * i;

@@ -414,10 +414,89 @@ static hipError_t pack_t(const void *chw, const void *gx, const void *gy, int C,
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// hwc_kernel: the FMPNP_LAYOUT_F pack -- a channels-last copy [C][H][W] -> [H][W][cstride]
+// fp32, padding channels zero-filled.  A workgroup moves one tile of HC_CT channels x HC_XT
+// columns of one row through LDS: 128-byte row segments in (8 lanes x 16 B per channel
+// row), 512-byte texel segments out (32 lanes x 16 B of consecutive channels per column,
+// nt stores), i.e. 8C bytes per texel of HBM traffic and no gradient work.
+constexpr int HC_CT = 128, HC_XT = 32, HC_NT = 256;
+constexpr int HC_LD = HC_XT + 1;  // odd row stride of the [channel][column] LDS tile
+
+template <typename Tin>
+__global__ __launch_bounds__(HC_NT) void hwc_kernel(const Tin *__restrict__ chw, int C, int H, int W,
+                                                  float *__restrict__ out, int cs, int nct, int nxt, int vec_ok) {
+    __shared__ float tile[HC_CT * HC_LD];
+    int b = blockIdx.x;
+    const int ct = b % nct;
+    b /= nct;
+    const int xt = b % nxt, y = b / nxt;
+    const int c0 = ct * HC_CT, x0 = xt * HC_XT;
+    const bool full_x = x0 + HC_XT <= W;
+    constexpr int QPR = HC_XT / 4;  // 16-byte (4-column) units per channel row
+    for (int i = threadIdx.x; i < HC_CT * QPR; i += HC_NT) {
+        const int cc = i / QPR, q = i - cc * QPR;
+        const int c = c0 + cc, x = x0 + 4 * q;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        if (c < C) {
+            const Tin *src = chw + ((size_t)c * H + y) * W + x;
+            if (vec_ok && full_x) {
+                if constexpr (sizeof(Tin) == 4) {
+                    const float4 w = *reinterpret_cast<const float4 *>(src);
+                    v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
+                } else {
+                    const double2 w0 = *reinterpret_cast<const double2 *>(src);
+                    const double2 w1 = *reinterpret_cast<const double2 *>(src + 2);
+                    v[0] = (float)w0.x; v[1] = (float)w0.y; v[2] = (float)w1.x; v[3] = (float)w1.y;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (x + k < W) v[k] = (float)src[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tile[cc * HC_LD + 4 * q + k] = v[k];
+    }
+    __syncthreads();
+    constexpr int QPC = HC_CT / 4;  // 16-byte (4-channel) units per column
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    for (int i = threadIdx.x; i < HC_XT * QPC; i += HC_NT) {
+        const int xx = i / QPC, cq = i - xx * QPC;
+        const int x = x0 + xx, c = c0 + 4 * cq;
+        if (x < W && c < cs) {
+            f4 o;
+            o.x = tile[(4 * cq + 0) * HC_LD + xx];
+            o.y = tile[(4 * cq + 1) * HC_LD + xx];
+            o.z = tile[(4 * cq + 2) * HC_LD + xx];
+            o.w = tile[(4 * cq + 3) * HC_LD + xx];
+            __builtin_nontemporal_store(o, reinterpret_cast<f4 *>(out + ((size_t)y * W + x) * cs + c));
+        }
+    }
+}
+
+template <typename Tin>
+static hipError_t hwc_t(const void *chw, int C, int H, int W, void *out, int cs, hipStream_t stream) {
+    const int nct = (cs + HC_CT - 1) / HC_CT, nxt = (W + HC_XT - 1) / HC_XT;
+    const long grid = (long)nct * nxt * H;
+    if (grid >= (1L << 31) || cs % 4 != 0 || ((uintptr_t)out % 16) != 0) return hipErrorInvalidValue;
+    const int vec_ok = ((uintptr_t)chw % 16 == 0) && ((size_t)W * sizeof(Tin)) % 16 == 0;
+    hipLaunchKernelGGL((hwc_kernel<Tin>), dim3((unsigned)grid), dim3(HC_NT), 0, stream, (const Tin *)chw, C, H, W,
+                       (float *)out, cs, nct, nxt, vec_ok);
+    return hipGetLastError();
+}
+
 hipError_t launch_pack(const void *chw, const void *gx, const void *gy, int dtype_in, int C, int H, int W, void *out,
                        int dtype_out, int cs, int normalized, int replicate, hipStream_t stream, int planes) {
     const bool grad = planes != 1;
     if (!grad && gx) return hipErrorInvalidValue;
+    if (!grad) {  // FMPNP_LAYOUT_F: fp32 channels-last copy (FMPNP_PACK_F_SOBEL=1: the Sobel kernel's f-only mode)
+        static const int via_sobel = [] { const char *e = getenv("FMPNP_PACK_F_SOBEL"); return e && *e == '1'; }();
+        if (dtype_out != FMPNP_F32) return hipErrorInvalidValue;
+        if (!via_sobel)
+            return dtype_in == FMPNP_F32 ? hwc_t<float>(chw, C, H, W, out, cs, stream)
+                                         : hwc_t<double>(chw, C, H, W, out, cs, stream);
+    }
     if (dtype_in == FMPNP_F32 && dtype_out == FMPNP_F32)
         return pack_t<float, float>(chw, gx, gy, C, H, W, out, cs, normalized, replicate, grad, stream);
     if (dtype_in == FMPNP_F32 && dtype_out == FMPNP_F64)

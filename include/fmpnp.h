@@ -147,8 +147,9 @@ int fmpnp_pack_features(const void *chw, const void *gx_chw, const void *gy_chw,
                         int W, void *out, int dtype_out, int cstride, int sobel_normalized,
                         int sobel_replicate_pad, void *hip_stream);
 
-/* Channels-last copy of f only, [H][W][cstride] (dtype_out): the FMPNP_LAYOUT_F input of
- * the LM kernel, a third of fmpnp_pack_features' output bytes. */
+/* Channels-last copy of f only, [H][W][cstride] fp32 (dtype_out = FMPNP_F32, cstride a
+ * multiple of 4, out 16-byte aligned; channels [C, cstride) zero-filled): the
+ * FMPNP_LAYOUT_F input of the LM kernel, a third of fmpnp_pack_features' output bytes. */
 int fmpnp_pack_features_f(const void *chw, int dtype_in, int C, int H, int W, void *out, int dtype_out,
                           int cstride, void *hip_stream);
 
