@@ -54,6 +54,7 @@ class RefinePipeline:
         loss_code, alpha = _losses.resolve(kw["loss_fn"])
         self.options = _rf.make_options(kw["n_iters"], kw["lambda_"], loss_code, alpha, kw.get("ratio_threshold"),
                                         _rf._dtype_code(storage), sampling=sampling)
+        self.sampling = sampling
         self.depth = max(1, int(depth))
         # "f" (f plane only, gradients formed in the LM gather) wherever it applies: fp32
         # texels, nearest sampling; "fgrad" (the packed f, gx, gy planes) otherwise
@@ -61,6 +62,8 @@ class RefinePipeline:
         self.layout = layout or ("f" if f_ok else "fgrad")
         if self.layout == "f" and not f_ok:
             raise ValueError("layout 'f' needs fp32 storage and nearest sampling")
+        self.bound_options = _lib.Options.from_buffer_copy(self.options)
+        self.bound_options.layout = _lib.LAYOUT_F if self.layout == "f" else _lib.LAYOUT_FGRAD
         self.prep, self.solve = _streams(self.device)
         self.slabs = [None] * self.depth        # flat uint8 device buffers holding a batch's packed maps
         self.slab_free = [None] * self.depth    # event: the last launch that read the slab finished
@@ -77,80 +80,82 @@ class RefinePipeline:
 
     def _prepare(self, queries, k):
         """Pack + gather every query of a batch on the prep stream into slab k: one batched
-        C-ABI call each for the Sobel packs and the reference gathers (no per-query host
-        round trips)."""
+        C-ABI call each for the packs and the reference gathers, and the LM descriptors
+        filled column-wise (no per-query host objects)."""
         dev, storage = self.device, self.storage
         nq = len(queries)
         qmaps = [q if q.dim() == 3 else q[0] for (q, _, _, _) in queries]
         rmaps = [r if r.dim() == 3 else r[0] for (_, r, _, _) in queries]
-        q_dt = qmaps[0].dtype if qmaps and qmaps[0].dtype in (torch.float32, torch.float64) else torch.float32
-        r_dt = rmaps[0].dtype if rmaps and rmaps[0].dtype in (torch.float32, torch.float64) else torch.float32
-        es = torch.empty(0, dtype=storage).element_size()
+        q_dt = qmaps[0].dtype if qmaps[0].dtype in (torch.float32, torch.float64) else torch.float32
+        r_dt = rmaps[0].dtype if rmaps[0].dtype in (torch.float32, torch.float64) else torch.float32
+        es = 4 if storage == torch.float32 else 8
         planes = 3 if self.layout == "fgrad" else 1
-        shapes = [(m.shape[1], m.shape[2], planes, _rf._round4(m.shape[0])) for m in qmaps]
-        sizes = [int(np.prod(sh)) * es for sh in shapes]
-        starts = np.concatenate([[0], np.cumsum([(b + _ALIGN - 1) // _ALIGN * _ALIGN for b in sizes])]).astype(int)
-        inl = [np.asarray(p.reference_inliers, np.float64).reshape(-1, 2) for (_, _, p, _) in queries]
-        pts = [np.asarray(p.points_3d, np.float64).reshape(-1, 3) for (_, _, p, _) in queries]
-        n_pts = [a.shape[0] for a in inl]
-        probs = []
+        Cs = np.array([m.shape[0] for m in qmaps], dtype=np.int64)
+        Hs = np.array([m.shape[1] for m in qmaps], dtype=np.int64)
+        Ws = np.array([m.shape[2] for m in qmaps], dtype=np.int64)
+        css = (Cs + 3) // 4 * 4
+        sizes = Hs * Ws * planes * css * es
+        starts = np.concatenate([[0], np.cumsum((sizes + _ALIGN - 1) // _ALIGN * _ALIGN)])
+        inl = [np.asarray(q[2].reference_inliers, np.float64).reshape(-1, 2) for q in queries]
+        pts = [np.asarray(q[2].points_3d, np.float64).reshape(-1, 3) for q in queries]
+        n_pts = np.array([a.shape[0] for a in inl], dtype=np.int64)
+        fr_off = np.concatenate([[0], np.cumsum(n_pts * css)])
         with torch.cuda.device(dev), torch.cuda.stream(self.prep):
-            qmaps = [_rf._as_device(m, dev, q_dt) for m in qmaps]   # no-ops for device maps of the batch dtype
-            rmaps = [_rf._as_device(m, dev, r_dt) for m in rmaps]
+            def ready(m, dt):  # device, batch dtype, contiguous (else one conversion copy)
+                return m if (m.is_cuda and m.dtype == dt and m.is_contiguous()) else _rf._as_device(m, dev, dt)
+            qmaps = [ready(m, q_dt) for m in qmaps]
+            rmaps = [ready(m, r_dt) for m in rmaps]
             slab = self._slab(k, max(int(starts[-1]), 1))
-            outs = [slab[starts[i]:starts[i] + sizes[i]].view(storage).view(shapes[i] if planes == 3 else
-                                                                              (shapes[i][0], shapes[i][1],
-                                                                               shapes[i][3]))
-                    for i in range(nq)]
-            for i in range(nq):
-                if shapes[i][3] != qmaps[i].shape[0]:
-                    outs[i].zero_()  # padding channels stay zero (the kernel writes c < C only)
+            out_ptrs = slab.data_ptr() + starts[:-1]
+            if planes == 3 and (css != Cs).any():  # the Sobel pack writes channels < C only
+                for i in np.nonzero(css != Cs)[0]:
+                    slab[int(starts[i]):int(starts[i] + sizes[i])].zero_()
             # one out-of-map flag per query, read once the batch finished (no host wait here)
             err = torch.zeros(nq, dtype=torch.int32, device=dev)
             # every query's reference inliers and 3D points in one pinned upload
-            flat = np.concatenate([a.reshape(-1) for a in inl + pts]) if nq else np.zeros(0)
+            flat = np.concatenate([a.reshape(-1) for a in inl + pts])
             dflat = torch.from_numpy(flat).pin_memory().to(dev, non_blocking=True)
-            offs = np.concatenate([[0], np.cumsum([a.size for a in inl + pts])]).astype(int)
+            offs = np.concatenate([[0], np.cumsum([a.size for a in inl + pts])])
             # reference descriptors of the whole batch: [N_i][cstride_i] runs in one buffer
-            fr_off = np.concatenate([[0], np.cumsum([n_pts[i] * shapes[i][3] for i in range(nq)])]).astype(int)
-            pad = any(shapes[i][3] != rmaps[i].shape[0] for i in range(nq))
+            pad = any(int(css[i]) != rmaps[i].shape[0] for i in range(nq))
             fbuf = (torch.zeros if pad else torch.empty)(max(int(fr_off[-1]), 1), dtype=storage, device=dev)
-            frefs = [fbuf[fr_off[i]:fr_off[i + 1]].view(n_pts[i], shapes[i][3]) for i in range(nq)]
+            fr_ptrs = fbuf.data_ptr() + es * fr_off[:-1]
             L = _lib.load()
             vp = ctypes.c_void_p
             s = _lib.stream_ptr(dev)
-            shape_arr = (ctypes.c_int * (4 * nq))(*[v for i in range(nq) for v in
-                                                    (qmaps[i].shape[0], shapes[i][0], shapes[i][1], shapes[i][3])])
+            shape_arr = (ctypes.c_int * (4 * nq))(*np.stack([Cs, Hs, Ws, css], 1).reshape(-1).tolist())
             rc = L.fmpnp_pack_features_batch(
-                nq, (vp * nq)(*[m.data_ptr() for m in qmaps]), (vp * nq)(*[o.data_ptr() for o in outs]), shape_arr,
+                nq, (vp * nq)(*[m.data_ptr() for m in qmaps]), (vp * nq)(*out_ptrs.tolist()), shape_arr,
                 _rf._dtype_code(q_dt), _rf._dtype_code(storage), 0, 0,
                 _lib.LAYOUT_F if self.layout == "f" else _lib.LAYOUT_FGRAD, s)                # :57, :61
             _lib.check(rc, "fmpnp_pack_features_batch")
             rshape = (ctypes.c_int * (3 * nq))(*[v for m in rmaps for v in m.shape])
             base = dflat.data_ptr()
             rc = L.fmpnp_gather_reference_batch(
-                nq, (vp * nq)(*[m.data_ptr() for m in rmaps]), rshape,
-                (vp * nq)(*[base + 8 * int(offs[i]) for i in range(nq)]), (ctypes.c_int * nq)(*n_pts),
-                int(self.image_shape[0]), int(self.image_shape[1]), (vp * nq)(*[f.data_ptr() for f in frefs]),
-                (ctypes.c_int * nq)(*[sh[3] for sh in shapes]), _rf._dtype_code(r_dt), _rf._dtype_code(storage),
-                vp(err.data_ptr()), s)                                                        # :51-56
+                nq, (vp * nq)(*[m.data_ptr() for m in rmaps]), rshape, (vp * nq)(*(base + 8 * offs[:nq]).tolist()),
+                (ctypes.c_int * nq)(*n_pts.tolist()), int(self.image_shape[0]), int(self.image_shape[1]),
+                (vp * nq)(*fr_ptrs.tolist()), (ctypes.c_int * nq)(*css.tolist()), _rf._dtype_code(r_dt),
+                _rf._dtype_code(storage), vp(err.data_ptr()), s)                               # :51-56
             _lib.check(rc, "fmpnp_gather_reference_batch")
-            for i, (_, _, pred, K) in enumerate(queries):
-                feats = _rf.PackedFeatures(outs[i], qmaps[i].shape[0], shapes[i][0], shapes[i][1], shapes[i][3],
-                                           self.layout, 0)
-                T = np.asarray(pred.matrix, dtype=np.float64)
-                probs.append(_rf.make_problem(feats, frefs[i], dflat[offs[nq + i]:offs[nq + i + 1]].view(-1, 3),
-                                              np.asarray(K, np.float64).reshape(3, 3), self.image_shape[0],
-                                              self.image_shape[1], T[:3, :3], T[:3, 3]))     # :52, :59-60
-            batch = _rf.AsyncBatch(probs, self.options, non_blocking=True)
-        # the maps are read on the prep stream only; keep them (and any converted copies)
-        # alive until the batch is collected
-        return batch, probs + [qmaps, rmaps, fbuf], err
+            # LM descriptors, column by column (fmpnp_problem)
+            desc = np.zeros(nq, dtype=_rf.PROBLEM_DTYPE)
+            desc["feat"], desc["fref"], desc["pts3d"] = out_ptrs, fr_ptrs, base + 8 * offs[nq:2 * nq]
+            desc["Hf"], desc["Wf"], desc["cstride"] = Hs, Ws, css
+            desc["c_end"], desc["ld_ref"], desc["N"] = Cs, css, n_pts
+            desc["im_width"], desc["im_height"] = int(self.image_shape[0]), int(self.image_shape[1])   # :52
+            T = np.stack([np.asarray(q[2].matrix, np.float64) for q in queries])                    # :59-60
+            desc["K"] = np.stack([np.asarray(q[3], np.float64).reshape(9) for q in queries])
+            desc["R0"] = T[:, :3, :3].reshape(nq, 9)
+            desc["t0"] = T[:, :3, 3]
+            batch = _rf.AsyncBatch.from_descriptors(desc, self.bound_options, dev, non_blocking=True)
+        # read on the prep stream (maps, converted copies) or the solve stream (the rest):
+        # kept alive until the batch is collected
+        return batch, [qmaps, rmaps, fbuf, dflat], err
 
     def run(self, batches):
         """batches: iterable of lists of queries.  Returns a list (per batch) of result dicts
         (see refine.refine), computed with preparation and refinement overlapped."""
-        inflight = []   # (batch, probs, err flags, done event) in submission order
+        inflight = []   # (batch, keep-alive buffers, err flags, done event) in submission order
         out = []
 
         def finish(entry):
@@ -167,24 +172,20 @@ class RefinePipeline:
             while len(inflight) >= self.depth:
                 finish(inflight.pop(0))
             k = i % self.depth
-            batch, probs, err = self._prepare(list(queries), k)
+            batch, keep, err = self._prepare(list(queries), k)
             ready = torch.cuda.Event()
             ready.record(self.prep)
             self.solve.wait_event(ready)
             with torch.cuda.device(self.device), torch.cuda.stream(self.solve):
                 batch.launch(_lib.stream_ptr(self.device))
                 # buffers written on the prep stream and read on the solve stream
-                for p in probs:
-                    if isinstance(p, _rf.Problem):
-                        p.fref.record_stream(self.solve)
-                        p.pts3d.record_stream(self.solve)
-                for t in (batch.d_descs, batch.d_res, batch.d_ws, err, self.slabs[k]):
+                for t in (batch.d_descs, batch.d_res, batch.d_ws, err, self.slabs[k], keep[2], keep[3]):
                     t.record_stream(self.solve)
             done = torch.cuda.Event()
             done.record(self.solve)
             self.slab_free[k] = done
-            inflight.append((batch, probs, err, done))
-            del batch, probs, err
+            inflight.append((batch, keep, err, done))
+            del batch, keep, err
         for entry in inflight:
             finish(entry)
         return out

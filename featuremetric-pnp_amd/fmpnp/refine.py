@@ -322,30 +322,62 @@ def refine(problems, options, trace=False):
     return results, traces
 
 
+PROBLEM_DTYPE = np.dtype(_lib.Problem)   # fmpnp_problem as a numpy structured dtype (same layout)
+RESULT_DTYPE = np.dtype(_lib.Result)
+
+
+def results_from_array(arr):
+    """fmpnp_result records (RESULT_DTYPE array) -> result dicts (as refine() returns)."""
+    R, t = arr["R"].reshape(-1, 3, 3), arr["t"]
+    cols = {k: arr[k].tolist() for k in ("initial_cost", "best_cost", "final_lambda", "final_lr", "best_num_inliers",
+                                          "n_evals", "n_steps", "n_accepted", "status", "has_best", "texel_gathers")}
+    return [dict(R=R[i].copy(), t=t[i].copy(), initial_cost=cols["initial_cost"][i], best_cost=cols["best_cost"][i],
+                 final_lambda=cols["final_lambda"][i], final_lr=cols["final_lr"][i],
+                 best_num_inliers=cols["best_num_inliers"][i], n_evals=cols["n_evals"][i],
+                 n_steps=cols["n_steps"][i], n_accepted=cols["n_accepted"][i], status=cols["status"][i],
+                 has_best=bool(cols["has_best"][i]), texel_gathers=int(cols["texel_gathers"][i]))
+            for i in range(len(arr))]
+
+
 class AsyncBatch:
     """Device-resident descriptors/results/workspace for repeated asynchronous launches
-    (the bench's timed region: nothing but the LM kernel and its counter memset)."""
+    (the bench's timed region: nothing but the LM kernel and its counter memset).
+
+    Built from Problem objects, or (`from_descriptors`) from an fmpnp_problem array the
+    caller filled column-wise -- the streamed pipeline's path, no per-query objects."""
 
     def __init__(self, problems, options, non_blocking=False):
         self.problems = list(problems)
-        self.options = bind_layout(self.problems, options)
-        n = len(self.problems)
-        self.n = n
-        self.dev = self.problems[0].feats.buf.device
+        desc = np.zeros(len(self.problems), dtype=PROBLEM_DTYPE)
+        for i, p in enumerate(self.problems):
+            d = p.descriptor()
+            desc[i] = np.frombuffer(ctypes.string_at(ctypes.addressof(d), PROBLEM_DTYPE.itemsize), PROBLEM_DTYPE)[0]
+        self._setup(desc, bind_layout(self.problems, options), self.problems[0].feats.buf.device, non_blocking)
+
+    @classmethod
+    def from_descriptors(cls, desc, options, device, non_blocking=False):
+        self = cls.__new__(cls)
+        self.problems = []
+        self._setup(desc, options, torch.device(device), non_blocking)
+        return self
+
+    def _setup(self, desc, options, dev, non_blocking):
+        self.options = options
+        self.n = n = len(desc)
+        self.dev = dev
         _lib.require_device(self.dev)
-        self.descs_host = (_lib.Problem * n)(*[p.descriptor() for p in self.problems])
-        nbytes = ctypes.sizeof(_lib.Problem) * n
-        self.d_descs = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
-        host = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(self.descs_host), nbytes)),
-                                dtype=torch.uint8)
+        self.descs_np = np.ascontiguousarray(desc)
+        self.descs_host = self.descs_np.ctypes.data_as(ctypes.POINTER(_lib.Problem))
+        host = torch.from_numpy(self.descs_np.view(np.uint8))
+        self.d_descs = torch.empty(host.numel(), dtype=torch.uint8, device=self.dev)
         self.d_descs.copy_(host.pin_memory() if non_blocking else host, non_blocking=non_blocking)
-        self.d_res = torch.zeros(ctypes.sizeof(_lib.Result) * n, dtype=torch.uint8, device=self.dev)
+        self.d_res = torch.zeros(RESULT_DTYPE.itemsize * n, dtype=torch.uint8, device=self.dev)
         ws = _lib.load().fmpnp_workspace_size(self.descs_host, n, ctypes.byref(self.options))
         if ws == 0:
             raise _lib.FmpnpError("fmpnp_workspace_size failed (invalid problems/options)")
         self.d_ws = torch.empty(ws, dtype=torch.uint8, device=self.dev)
         self.ws_bytes = ws
-        self.max_n = max(p.pts3d.shape[0] for p in self.problems)
+        self.max_n = int(self.descs_np["N"].max()) if n else 0
 
     def launch(self, stream=None):
         s = stream if stream is not None else _lib.stream_ptr(self.dev)
@@ -357,9 +389,7 @@ class AsyncBatch:
 
     def results(self):
         torch.cuda.current_stream(self.dev).synchronize()
-        raw = bytes(self.d_res.cpu().numpy().tobytes())
-        arr = (_lib.Result * self.n).from_buffer_copy(raw)
-        return [_result_dict(r) for r in arr]
+        return results_from_array(self.d_res.cpu().numpy().view(RESULT_DTYPE))
 
 
 def project_pixels(R, t, pts3d, K):
