@@ -753,12 +753,9 @@ __device__ __forceinline__ void gather_pipe(unsigned long long m, int off, bool 
 // rounding the packed gradients carry.  Channel order and zero-filled second rounds as in
 // gather_half, so the sums do not depend on where the point sits.
 // ---------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ void sobel_acc(double a[8], const T *tap[9], int e, const T *pr, bool mask,
-                                          const bool ok[9], bool norm, bool zero) {
-    double v[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) v[k] = (zero || (mask && !ok[k])) ? 0.0 : (double)tap[k][e];
+// One channel: the 3x3 values v (rows above / at / below x columns left / at / right),
+// gradients by the separable form, then the six sums.
+__device__ __forceinline__ void sobel_acc_v(double a[8], const double v[9], double r, bool norm) {
     const double sxm = (v[0] + 2.0 * v[3]) + v[6], sym = v[6] - v[0];
     const double sy0 = v[7] - v[1];
     const double sxp = (v[2] + 2.0 * v[5]) + v[8], syp = v[8] - v[2];
@@ -767,9 +764,19 @@ __device__ __forceinline__ void sobel_acc(double a[8], const T *tap[9], int e, c
         gx *= 0.125;
         gy *= 0.125;
     }
-    acc6(a, v[4], zero ? 0.0 : (double)pr[e], gx, gy);
+    acc6(a, v[4], r, gx, gy);
 }
 
+// Element e of the nine tap vectors (and of fref): zero = the lane's channel lies past the
+// slice, mask = the point's neighbourhood is cut by the map edge (ok[k] false: a zero tap).
+template <typename T>
+__device__ __forceinline__ void sobel_acc(double a[8], const T *tap[9], int e, const T *pr, bool mask,
+                                          const bool ok[9], bool norm, bool zero) {
+    double v[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) v[k] = (zero || (mask && !ok[k])) ? 0.0 : (double)tap[k][e];
+    sobel_acc_v(a, v, zero ? 0.0 : (double)pr[e], norm);
+}
 // One point per trip, the whole wave on its channels (lane l: channels cb + l V + r 64 V):
 // the nine tap addresses and border masks are wave-uniform (scalar registers), ten 16-byte
 // loads per lane per round.
@@ -804,6 +811,92 @@ __device__ __forceinline__ void gather_f_point(const T *__restrict__ feat, const
                 sobel_acc<T>(a, tap, 0, rf + chs, MASK, ok, norm, !in);
             }
         }
+    }
+}
+
+// One trip's state for the double-buffered form (one channel round, 16-byte loads): the
+// point, its nine tap loads, fref, and its (wave-uniform) border masks.
+template <typename T>
+struct FTrip {
+    typename V16<T>::type x[9], q;
+    int p;
+    bool ok[9], interior;
+};
+
+__device__ __forceinline__ void f_taps(int prc, int Hf, int Wf, bool rep, int o[9], bool ok[9], bool &interior) {
+    const int row = prc >> 16, col = prc & 0xffff;
+#pragma unroll
+    for (int dr = 0; dr < 3; ++dr)
+#pragma unroll
+        for (int dc = 0; dc < 3; ++dc) {
+            const int r = row + dr - 1, c = col + dc - 1;
+            const int rr = min(max(r, 0), Hf - 1), cc = min(max(c, 0), Wf - 1);
+            o[3 * dr + dc] = rr * Wf + cc;
+            ok[3 * dr + dc] = rep || (r == rr && c == cc);
+        }
+    interior = rep || (row > 0 && row < Hf - 1 && col > 0 && col < Wf - 1);
+}
+
+template <typename T>
+__device__ __forceinline__ void f_issue(FTrip<T> &tr, unsigned long long &m, int rc, const T *feat, const T *fref0,
+                                        int cs, int ld, int c, int Hf, int Wf, bool rep) {
+    using VT = typename V16<T>::type;
+    tr.p = __builtin_ctzll(m);
+    m &= m - 1;
+    int o[9];
+    f_taps(__builtin_amdgcn_readlane(rc, tr.p), Hf, Wf, rep, o, tr.ok, tr.interior);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) tr.x[k] = gload<VT>(feat + (size_t)o[k] * cs + c);
+    tr.q = gload<VT>(fref0 + (size_t)tr.p * ld + c);
+}
+
+template <typename T, bool FULL>
+__device__ __forceinline__ void f_consume(const FTrip<T> &tr, bool has, bool norm, int lane, double *rec0, int e6,
+                                          bool wlane) {
+    constexpr int V = V16<T>::n;
+    double a[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = 0.0;
+    const T *t[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) t[k] = reinterpret_cast<const T *>(&tr.x[k]);
+    const T *pq = reinterpret_cast<const T *>(&tr.q);
+    if (tr.interior) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) sobel_acc<T>(a, t, e, pq, false, tr.ok, norm, !has);
+    } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) sobel_acc<T>(a, t, e, pq, true, tr.ok, norm, !has);
+    }
+    double r = reduce8_in32(a, lane), r2 = r;
+    swap32(r, r2);
+    r = r + r2;
+    if (wlane && lane < 32) rec0[(size_t)tr.p * RECW + e6] = r;
+}
+
+// Double-buffered form for C <= 64 V with 16-byte loads (one channel round per lane): the
+// next point's ten loads are in flight while this point's sums are formed and reduced.
+// Same per-lane arithmetic as gather_f_point, so the records are identical.
+template <typename T, bool FULL>
+__device__ __forceinline__ void gather_f_pipe(unsigned long long m, int rc, int lane, const T *feat, const T *fref0,
+                                              int cs, int cb, int ce, int ld, int Hf, int Wf, bool norm, bool rep,
+                                              double *rec0, int e6, bool wlane) {
+    constexpr int V = V16<T>::n;
+    if (!m) return;
+    const int c0 = cb + lane * V;
+    const bool has = c0 < ce;
+    const int c = has ? c0 : cb;  // lanes past the slice read (and zero) the first vector
+    FTrip<T> A, B;
+    f_issue<T>(A, m, rc, feat, fref0, cs, ld, c, Hf, Wf, rep);
+    while (true) {
+        const bool moreB = m != 0;
+        if (moreB) f_issue<T>(B, m, rc, feat, fref0, cs, ld, c, Hf, Wf, rep);
+        f_consume<T, FULL>(A, has, norm, lane, rec0, e6, wlane);
+        if (!moreB) break;
+        const bool moreA = m != 0;
+        if (moreA) f_issue<T>(A, m, rc, feat, fref0, cs, ld, c, Hf, Wf, rep);
+        f_consume<T, FULL>(B, has, norm, lane, rec0, e6, wlane);
+        if (!moreA) break;
     }
 }
 
@@ -912,8 +1005,12 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
         const bool wlane = (lane & 3) == 0 && e6 < 6;
         if constexpr (FL) {
-            gather_f_block<T>(m, rc, hi, lane, feat, fref + (size_t)(p0 + blk * 64) * ld, cs, cb, ce, ld, q.Hf, q.Wf,
-                              vec, q.sob_norm != 0, q.sob_rep != 0, rec + (size_t)blk * 64 * RECW, e6, wlane);
+            if (PIPE && vec && ce - cb <= 64 * V)  // one channel round per lane
+                gather_f_pipe<T, true>(m, rc, lane, feat, fref + (size_t)(p0 + blk * 64) * ld, cs, cb, ce, ld, q.Hf,
+                                       q.Wf, q.sob_norm != 0, q.sob_rep != 0, rec + (size_t)blk * 64 * RECW, e6, wlane);
+            else
+                gather_f_block<T>(m, rc, hi, lane, feat, fref + (size_t)(p0 + blk * 64) * ld, cs, cb, ce, ld, q.Hf,
+                                  q.Wf, vec, q.sob_norm != 0, q.sob_rep != 0, rec + (size_t)blk * 64 * RECW, e6, wlane);
         } else if (q.bilinear) {
             gather_bil_block<T>(m, tp, hi, lane, feat, fref + (size_t)(p0 + blk * 64) * ld, cs, cb, ce, ld, vec,
                                 rec + (size_t)blk * 64 * RECW, e6, wlane);

@@ -7,11 +7,12 @@ from fmpnp import _lib, refine as rf, synth
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 wgs = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+layout = sys.argv[3] if len(sys.argv) > 3 else "fgrad"   # "f": FMPNP_LAYOUT_F
 dev = torch.device("cuda", 0)
 probs = []
 for q in range(B):
     inp = synth.problem_inputs(512, 256, 240, 320, seed=q, device=dev)
-    feats = rf.pack_features(inp["fmap"], storage=torch.float32, device=dev)
+    feats = rf.pack_features(inp["fmap"], storage=torch.float32, device=dev, layout=layout)
     probs.append(rf.make_problem(feats, inp["fref"], inp["pts3d"], inp["K"], inp["im_width"], inp["im_height"], inp["R0"], inp["t0"]))
 opts = rf.make_options(50, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32, wgs_per_problem=wgs)
 ab = rf.AsyncBatch(probs, opts)
