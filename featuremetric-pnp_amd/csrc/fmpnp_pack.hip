@@ -420,12 +420,12 @@ static hipError_t pack_t(const void *chw, const void *gx, const void *gy, int C,
 // columns of one row through LDS: 128-byte row segments in (8 lanes x 16 B per channel
 // row), 512-byte texel segments out (32 lanes x 16 B of consecutive channels per column,
 // nt stores), i.e. 8C bytes per texel of HBM traffic and no gradient work.
-constexpr int HC_CT = 128, HC_XT = 32, HC_NT = 256;
-constexpr int HC_LD = HC_XT + 1;  // odd row stride of the [channel][column] LDS tile
+constexpr int HC_NT = 256;
 
-template <typename Tin>
+template <typename Tin, int HC_CT, int HC_XT>
 __global__ __launch_bounds__(HC_NT) void hwc_kernel(const Tin *__restrict__ chw, int C, int H, int W,
                                                   float *__restrict__ out, int cs, int nct, int nxt, int vec_ok) {
+    constexpr int HC_LD = HC_XT + 1;  // odd row stride of the [channel][column] LDS tile
     __shared__ float tile[HC_CT * HC_LD];
     int b = blockIdx.x;
     const int ct = b % nct;
@@ -475,15 +475,25 @@ __global__ __launch_bounds__(HC_NT) void hwc_kernel(const Tin *__restrict__ chw,
     }
 }
 
-template <typename Tin>
-static hipError_t hwc_t(const void *chw, int C, int H, int W, void *out, int cs, hipStream_t stream) {
-    const int nct = (cs + HC_CT - 1) / HC_CT, nxt = (W + HC_XT - 1) / HC_XT;
+template <typename Tin, int CT, int XT>
+static hipError_t hwc_ct(const void *chw, int C, int H, int W, void *out, int cs, hipStream_t stream) {
+    const int nct = (cs + CT - 1) / CT, nxt = (W + XT - 1) / XT;
     const long grid = (long)nct * nxt * H;
     if (grid >= (1L << 31) || cs % 4 != 0 || ((uintptr_t)out % 16) != 0) return hipErrorInvalidValue;
     const int vec_ok = ((uintptr_t)chw % 16 == 0) && ((size_t)W * sizeof(Tin)) % 16 == 0;
-    hipLaunchKernelGGL((hwc_kernel<Tin>), dim3((unsigned)grid), dim3(HC_NT), 0, stream, (const Tin *)chw, C, H, W,
-                       (float *)out, cs, nct, nxt, vec_ok);
+    hipLaunchKernelGGL((hwc_kernel<Tin, CT, XT>), dim3((unsigned)grid), dim3(HC_NT), 0, stream, (const Tin *)chw, C, H,
+                       W, (float *)out, cs, nct, nxt, vec_ok);
     return hipGetLastError();
+}
+
+template <typename Tin>
+static hipError_t hwc_t(const void *chw, int C, int H, int W, void *out, int cs, hipStream_t stream) {
+    static const int ct = [] { const char *e = getenv("FMPNP_PACK_F_CT"); return e ? atoi(e) : 64; }();
+    static const int xt = [] { const char *e = getenv("FMPNP_PACK_F_XT"); return e ? atoi(e) : 32; }();
+    if (xt == 64) return ct == 128 ? hwc_ct<Tin, 128, 64>(chw, C, H, W, out, cs, stream)
+                                   : hwc_ct<Tin, 64, 64>(chw, C, H, W, out, cs, stream);
+    if (ct == 128) return hwc_ct<Tin, 128, 32>(chw, C, H, W, out, cs, stream);
+    return hwc_ct<Tin, 64, 32>(chw, C, H, W, out, cs, stream);
 }
 
 hipError_t launch_pack(const void *chw, const void *gx, const void *gy, int dtype_in, int C, int H, int W, void *out,
