@@ -266,12 +266,9 @@ int fmpnp_gather_reference_batch(int n, const void *const *ref_chw, const int *r
             !gather_args_ok(ref_chw[i], sh[0], sh[1], sh[2], ref_inliers[i], n_inliers[i], img0, img1, out[i], ld_out[i]))
             return FMPNP_EINVAL;
     }
-    for (int i = 0; i < n; ++i) {
-        if (n_inliers[i] == 0) continue;
-        const int *sh = ref_shape + 3 * i;
-        const hipError_t e = launch_gather_ref(ref_chw[i], dtype_in, sh[0], sh[1], sh[2], ref_inliers[i], n_inliers[i],
-                                               img0, img1, out[i], dtype_out, ld_out[i], err_flags + i,
-                                               (hipStream_t)hip_stream);
+    {
+        const hipError_t e = launch_gather_ref_batch(n, ref_chw, ref_shape, ref_inliers, n_inliers, img0, img1, out,
+                                                     ld_out, dtype_in, dtype_out, err_flags, (hipStream_t)hip_stream);
         if (e != hipSuccess) return (int)e;
     }
     return 0;

@@ -555,6 +555,94 @@ static hipError_t gather_t(const void *ref, int C, int H, int W, const double *i
     return hipGetLastError();
 }
 
+// Many queries' gathers in one launch (fmpnp_gather_reference_batch): the item table rides
+// in the kernel arguments, the grid strides over all items' (point, channel) elements --
+// one query's grid (512 x 256 elements at cfg2) is too small to hide the scattered CHW
+// reads' latency on its own.
+constexpr int GB_MAX = 32;
+struct GatherItems {
+    const void *ref[GB_MAX];
+    const double *inl[GB_MAX];
+    void *out[GB_MAX];
+    int C[GB_MAX], H[GB_MAX], W[GB_MAX], ld[GB_MAX];
+    long start[GB_MAX + 1];  // element offsets: item i owns [start[i], start[i+1]) (empty items allowed)
+    int n, img0, img1;
+    int *err;                // [n] flags
+};
+
+template <typename Tin, typename Tout>
+__global__ __launch_bounds__(PK_NT) void gather_ref_batch_kernel(GatherItems it) {
+    const long total = it.start[it.n];
+    for (long e = blockIdx.x * (long)PK_NT + threadIdx.x; e < total; e += (long)gridDim.x * PK_NT) {
+        int lo = 0, hi = it.n - 1;  // the last item whose range starts at or before e
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (it.start[mid] <= e) lo = mid;
+            else hi = mid - 1;
+        }
+        const int i = lo, C = it.C[i], H = it.H[i], W = it.W[i];
+        const long k = e - it.start[i];
+        const int n = (int)(k / C), c = (int)(k % C);
+        const double rel0 = (double)H / (double)it.img0, rel1 = (double)W / (double)it.img1;
+        const double *inl = it.inl[i];
+        const double x = inl[2 * n], y = inl[2 * n + 1];
+        const double colf = rel0 * x, rowf = rel1 * y;
+        int col = (int)colf, row = (int)rowf;  // as gather_ref_kernel
+        if (row < 0 && row >= -H) row += H;
+        if (col < 0 && col >= -W) col += W;
+        Tout *out = reinterpret_cast<Tout *>(it.out[i]) + (size_t)n * it.ld[i] + c;
+        if (row < 0 || row >= H || col < 0 || col >= W || !(colf == colf) || !(rowf == rowf)) {
+            if (c == 0) atomicOr(it.err + i, 1);
+            *out = (Tout)0;
+            continue;
+        }
+        *out = (Tout)reinterpret_cast<const Tin *>(it.ref[i])[((size_t)c * H + row) * W + col];
+    }
+}
+
+template <typename Tin, typename Tout>
+static hipError_t gather_batch_t(const GatherItems &it, hipStream_t stream) {
+    const long total = it.start[it.n];
+    long grid = (total + PK_NT - 1) / PK_NT;
+    if (grid > 8192) grid = 8192;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((gather_ref_batch_kernel<Tin, Tout>), dim3((unsigned)grid), dim3(PK_NT), 0, stream, it);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_ref_batch(int n, const void *const *ref, const int *ref_shape, const double *const *inl,
+                                   const int *n_inl, int img0, int img1, void *const *out, const int *ld_out,
+                                   int dtype_in, int dtype_out, int *err, hipStream_t stream) {
+    for (int i0 = 0; i0 < n; i0 += GB_MAX) {
+        GatherItems it{};
+        const int m = n - i0 < GB_MAX ? n - i0 : GB_MAX;
+        it.start[0] = 0;
+        for (int j = 0; j < m; ++j) {
+            const int i = i0 + j;
+            it.ref[j] = ref[i];
+            it.inl[j] = inl[i];
+            it.out[j] = out[i];
+            it.C[j] = ref_shape[3 * i];
+            it.H[j] = ref_shape[3 * i + 1];
+            it.W[j] = ref_shape[3 * i + 2];
+            it.ld[j] = ld_out[i];
+            it.start[j + 1] = it.start[j] + (long)n_inl[i] * it.C[j];
+        }
+        if (it.start[m] == 0) continue;
+        it.n = m;
+        it.img0 = img0;
+        it.img1 = img1;
+        it.err = err + i0;
+        hipError_t e;
+        if (dtype_in == FMPNP_F32 && dtype_out == FMPNP_F32) e = gather_batch_t<float, float>(it, stream);
+        else if (dtype_in == FMPNP_F32 && dtype_out == FMPNP_F64) e = gather_batch_t<float, double>(it, stream);
+        else if (dtype_in == FMPNP_F64 && dtype_out == FMPNP_F32) e = gather_batch_t<double, float>(it, stream);
+        else e = gather_batch_t<double, double>(it, stream);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 hipError_t launch_gather_ref(const void *ref, int dtype_in, int C, int H, int W, const double *inl, int N, int img0,
                              int img1, void *out, int dtype_out, int ld_out, int *err, hipStream_t stream) {
     if (dtype_in == FMPNP_F32 && dtype_out == FMPNP_F32)

@@ -57,3 +57,36 @@ def test_batched_pack_and_gather_equal_single_calls():
     for a, b in zip(expect, got):
         assert torch.equal(a, b)
     assert err.tolist() == [0, 0, 1]
+
+
+def test_batched_gather_with_empty_items_and_more_than_one_launch():
+    """40 items (two launches of the item table) with empty ones among them: every
+    non-empty item equals its single-call gather, empty items leave their flag at 0."""
+    import torch
+    from fmpnp import _lib, refine as rf
+    dev = torch.device("cuda", 0)
+    L = _lib.load()
+    vp = ctypes.c_void_p
+    g = torch.Generator().manual_seed(5)
+    rng = np.random.default_rng(6)
+    n = 40
+    refs = [torch.randn((16, 12, 12), generator=g).to(dev) for _ in range(n)]
+    counts = [0 if i % 7 == 3 else int(rng.integers(1, 20)) for i in range(n)]
+    inls = [torch.from_numpy(rng.uniform(0, 48, (max(c, 1), 2))).to(dev) for c in counts]
+    outs = [torch.zeros((max(c, 1), 16), device=dev) for c in counts]
+    err = torch.zeros(n, dtype=torch.int32, device=dev)
+    rc = L.fmpnp_gather_reference_batch(
+        n, (vp * n)(*[r.data_ptr() for r in refs]), (ctypes.c_int * (3 * n))(*[v for r in refs for v in r.shape]),
+        (vp * n)(*[a.data_ptr() for a in inls]), (ctypes.c_int * n)(*counts), 48, 48,
+        (vp * n)(*[o.data_ptr() for o in outs]), (ctypes.c_int * n)(*([16] * n)), _lib.F32, _lib.F32,
+        vp(err.data_ptr()), _lib.stream_ptr(dev))
+    _lib.check(rc, "gather batch")
+    torch.cuda.synchronize()
+    assert not err.any()
+    for i in range(n):
+        if counts[i] == 0:
+            assert not outs[i].any()
+            continue
+        one = rf.gather_reference(refs[i], inls[i].cpu().numpy(), (48, 48), cstride=16)
+        assert torch.equal(one, outs[i])
+
