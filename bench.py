@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=128, help="queries per GPU")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="total queries split over the GPUs (strong scaling); 0 = --batch per GPU (weak)")
     ap.add_argument("--wgs", type=int, default=0, help="workgroups per query (0 = auto)")
     ap.add_argument("--cpu-sample", type=int, default=1024, help="queries in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -82,7 +84,9 @@ def main():
     from fmpnp import _lib, refine as rf, synth
 
     # ---------------- setup (untimed): this rank's queries, packed in HBM ----------------
-    B = args.batch
+    # weak scaling (default): B queries per GPU; --global-batch G: G queries split over the
+    # ranks (SURVEY.md 8e's fixed-total form, e.g. 1024), strong scaling
+    B = -(-args.global_batch // world) if args.global_batch > 0 else args.batch
     t0 = time.time()
     probs = []
     keep = []
@@ -245,7 +249,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.global_batch > 0 else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SURVEY.md §8d: smoothed L2-normalised random hypercolumns, seeded points)",
