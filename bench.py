@@ -375,7 +375,7 @@ def run_extras(args, dev, probs, keep, opts, rf, _lib, synth):
     if not args.no_pipeline:
         import fmpnp
         from fmpnp.pipeline import RefinePipeline
-        nb, qb = 4, 32
+        nb, qb = 4, 64
         batches, img = synth.pipeline_queries(nb, qb, N_PTS, C, HF, WF, device=dev, seed0=5000)
         pipe = RefinePipeline(img, storage=torch.float32, depth=2,
                               model_kwargs=dict(n_iters=ITERS, loss_fn=fmpnp.geman_mcclure_loss, lambda_=0.01,
