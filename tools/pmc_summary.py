@@ -6,7 +6,9 @@ FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB.  On gfx950 FETCH_
 reports half of the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM section):
 it is doubled here; WRITE_SIZE is taken as is.
 
-usage: pmc_summary.py <prof_dir> <batch> <out.json>
+usage: pmc_summary.py <prof_dir> <batch> <out.json> [kernel name substring]
+(default: the benchmarked variant, lm_kernel<float, 2, false, false, 1>: fp32 texels, one
+workgroup per problem, no ratio test, Geman-McClure on the packed f/gx/gy layout)
 """
 import csv
 import glob
@@ -36,7 +38,7 @@ def counter_avg(prof, sub, name, kernel_key):
 
 def main():
     prof, batch, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
-    key = "lm_kernel"
+    key = sys.argv[4] if len(sys.argv) > 4 else "lm_kernel<float, 2, false, false, 1>"
     stats = [r for r in rows(os.path.join(prof, "trace", "**", "*kernel_stats.csv"))]
     lm = [r for r in stats if key in r.get("Name", "")]
     fetch_kib, nf = counter_avg(prof, "pmc_fetch", "FETCH_SIZE", key)
