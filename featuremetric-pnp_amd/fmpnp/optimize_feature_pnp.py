@@ -23,13 +23,20 @@ def _new_model(model):
 
 
 def feature_pnp(query_hypercolumns, reference_hypercolumns, prediction, K, image_shape, track=False,
-                feature_pyramid=None, model=None, storage=None):
-    """optimize_feature_pnp.py:50-71.  Returns (R, t, model) with R, t fp64 CPU tensors."""
+                feature_pyramid=None, model=None, storage=None, layout=None):
+    """optimize_feature_pnp.py:50-71.  Returns (R, t, model) with R, t fp64 CPU tensors.
+
+    layout: None picks the f-only layout (FMPNP_LAYOUT_F: the LM kernel forms the fp64 Sobel
+    gradients, a third of the pack's bytes) for fp32 texels with nearest sampling and no
+    pyramid, else the packed f/gx/gy planes ("fgrad")."""
     model = _new_model(model)
     q = query_hypercolumns[0] if query_hypercolumns.dim() == 4 else query_hypercolumns
     dev = q.device if q.is_cuda else torch.device("cuda", torch.cuda.current_device())
     storage = storage or model.storage or (torch.float64 if q.dtype == torch.float64 else torch.float32)
-    feats = _rf.pack_features(q, storage=storage, device=dev)                               # :57, :61
+    if layout is None:
+        layout = ("f" if storage == torch.float32 and feature_pyramid is None
+                  and getattr(model, "sampling", "nearest") == "nearest" else "fgrad")
+    feats = _rf.pack_features(q, storage=storage, device=dev, layout=layout)               # :57, :61
     fref = _rf.gather_reference(reference_hypercolumns, prediction.reference_inliers, image_shape,
                                 cstride=feats.cstride, storage=storage, device=dev)          # :51-56
     pts3D = np.asarray(prediction.points_3d, dtype=np.float64).reshape(-1, 3)               # :52

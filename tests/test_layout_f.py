@@ -158,3 +158,17 @@ def test_mixed_layouts_in_one_launch_are_refused():
                              inp["t0"]) for p in (pf, pg)]
     with pytest.raises(ValueError):
         rf.refine(probs, rf.make_options(3, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32))
+
+
+def test_facade_feature_pnp_fp32_takes_layout_f():
+    """feature_pnp on an fp32 hypercolumn packs f only (the default for fp32, nearest, no
+    pyramid) and lands where the fp64 packed-gradient path lands."""
+    ((query,),), img = synth.pipeline_queries(1, 1, N=256, C=64, Hf=60, Wf=80, device=DEV, seed0=77)
+    q, r, pred, K = query
+    Kt = torch.from_numpy(np.asarray(K, np.float64))
+    R32, t32, m32 = fmpnp.feature_pnp(q[None], r, pred, Kt, img)
+    R64, t64, m64 = fmpnp.feature_pnp(q[None], r, pred, Kt, img, storage=torch.float64)
+    assert rot_angle(R32.numpy(), R64.numpy()) < 1e-6
+    assert np.linalg.norm(t32.numpy() - t64.numpy()) < 1e-6
+    np.testing.assert_allclose(m32.best_cost_.item(), m64.best_cost_.item(), rtol=1e-9)
+    assert m32.best_num_inliers_ == m64.best_num_inliers_
