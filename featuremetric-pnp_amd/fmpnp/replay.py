@@ -15,8 +15,9 @@ Here:
     strings, `np.load(allow_pickle=False)`), the format this build replays from;
   * `prediction_from_entry` builds the reference's `Prediction` (same field names and
     inlier-mask application as :211-222);
-  * `replay` refines MANY queries in ONE device launch (the reference loops over
-    queries), with the same per-query preamble as `feature_pnp`
+  * `replay` refines many queries per device launch (the reference loops over
+    queries), streamed in batches through fmpnp.pipeline, with the same per-query
+    preamble as `feature_pnp`
     (optimize_feature_pnp.py:50-71: device Sobel + pack, truncating fref gather, fp64
     points, R/t from `prediction.matrix`), and returns per-query poses (t, quaternion as
     optimize_feature_pnp.py:84-91) and the reference's summary rows
@@ -33,7 +34,7 @@ import torch
 
 from . import _lib, config
 from . import losses as _losses
-from . import refine as _rf
+
 from .matrix_utils import matrix_quaternion
 
 # s2dhm/pose_prediction/solve_pnp.py:7-8
@@ -126,42 +127,43 @@ def _hc(source, name):
 
 
 def replay(entries, query_hc, reference_hc, K, image_shape=None, storage=torch.float32, device=None,
-           model_kwargs=None, sampling="nearest"):
-    """Refine every successful cached query in one launch.
+           model_kwargs=None, sampling="nearest", batch_size=128, depth=2):
+    """Refine every successful cached query, `batch_size` queries per device launch.
 
     entries: {key: entry dict} (read_cached_matches / load_flat).  query_hc / reference_hc:
-    dict or callable, image name -> hypercolumn.  K: 3x3 intrinsics, or a dict / callable
+    dict or callable, image name -> hypercolumn (loaded batch by batch, so a query set larger
+    than the device holds streams through).  K: 3x3 intrinsics, or a dict / callable
     query name -> K.  Returns (results, summary rows): results[key] = dict(t, quaternion, R,
     status, initial_cost, best_cost, best_num_inliers, n_evals); summary rows in
     SUMMARY_COLUMNS order.  Unsuccessful predictions are not refined (the reference only
     refines `best_prediction.success`, :239) and get an all-None summary row (:261).
+    The batches go through fmpnp.pipeline.RefinePipeline (per-query preamble of
+    feature_pnp, optimize_feature_pnp.py:50-71, on one stream under the previous batch's
+    LM launch on another).
     """
+    from .pipeline import RefinePipeline
     cfg = config.adapter_kwargs()
     image_shape = tuple(image_shape or cfg.get("image_shape", (1024, 1024)))
-    kw = config.model_kwargs()
-    kw.update(model_kwargs or {})
-    loss_code, alpha = _losses.resolve(kw["loss_fn"])
     device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     _lib.require_device(device)
-    keys, problems, preds = [], [], {}
-    for key, e in entries.items():
-        pred = prediction_from_entry(e)
-        preds[key] = pred
-        if not pred.success:
-            continue
-        q = query_name(key)
-        feats = _rf.pack_features(_hc(query_hc, q), storage=storage, device=device)          # :57, :61
-        fref = _rf.gather_reference(_hc(reference_hc, pred.reference_filename), pred.reference_inliers,
-                                    image_shape, cstride=feats.cstride, storage=storage, device=device)  # :51-56
-        Kq = K(q) if callable(K) else (K[q] if isinstance(K, dict) else K)
-        T = pred.matrix
-        problems.append(_rf.make_problem(feats, fref, np.asarray(pred.points_3d, np.float64).reshape(-1, 3),
-                                         np.asarray(Kq, np.float64).reshape(3, 3), image_shape[0], image_shape[1],
-                                         T[:3, :3], T[:3, 3]))                              # :52, :59-60
-        keys.append(key)
-    opts = _rf.make_options(kw["n_iters"], kw["lambda_"], loss_code, alpha, kw.get("ratio_threshold"),
-                            _rf._dtype_code(storage), sampling=sampling)
-    res, _ = _rf.refine(problems, opts) if problems else ([], None)
+    preds = {key: prediction_from_entry(e) for key, e in entries.items()}
+    keys = [key for key, pred in preds.items() if pred.success]
+    bs = max(1, int(batch_size))
+
+    def batches():
+        for i in range(0, len(keys), bs):
+            out = []
+            for key in keys[i:i + bs]:
+                pred, q = preds[key], query_name(key)
+                Kq = K(q) if callable(K) else (K[q] if isinstance(K, dict) else K)
+                out.append((_hc(query_hc, q), _hc(reference_hc, pred.reference_filename), pred, Kq))
+            yield out
+
+    res = []
+    if keys:
+        pipe = RefinePipeline(image_shape, storage=storage, device=device, depth=depth, model_kwargs=model_kwargs,
+                              sampling=sampling)
+        res = [r for b in pipe.run(batches()) for r in b]
     results, rows = {}, []
     by_key = dict(zip(keys, res))
     for key, pred in preds.items():

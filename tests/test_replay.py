@@ -96,7 +96,7 @@ def test_batched_replay_reproduces_reference_feature_pnp():
     q = torch.from_numpy(z["in_query"])[None]
     r = torch.from_numpy(z["in_ref"])[None]
     results, rows = rp.replay(entries, lambda name: q, {"ref.png": r}, z["in_K"], tuple(meta["image_shape"]),
-                              storage=torch.float64,
+                              storage=torch.float64, batch_size=2,   # three pipeline batches
                               model_kwargs=dict(n_iters=meta["n_iters"], loss_fn=fmpnp.geman_mcclure_loss,
                                                 lambda_=meta["lambda0"], ratio_threshold=None))
     assert len(results) == 5 and len(rows) == 6
