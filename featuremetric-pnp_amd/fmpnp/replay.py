@@ -34,7 +34,6 @@ import torch
 
 from . import _lib, config
 from . import losses as _losses
-
 from .matrix_utils import matrix_quaternion
 
 # s2dhm/pose_prediction/solve_pnp.py:7-8
