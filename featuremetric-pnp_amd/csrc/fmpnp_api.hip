@@ -243,6 +243,10 @@ int fmpnp_pack_features_batch(int n, const void *const *chw, void *const *out, c
         if (!chw[i] || !out[i] || sh[0] <= 0 || sh[1] <= 0 || sh[2] <= 0 || sh[3] < sh[0]) return FMPNP_EINVAL;
         if (layout == FMPNP_LAYOUT_F && (sh[3] % 4 || (uintptr_t)out[i] % 16)) return FMPNP_EINVAL;
     }
+    if (layout == FMPNP_LAYOUT_F) {  // one launch per 32 maps
+        static const int via_sobel = [] { const char *e = getenv("FMPNP_PACK_F_SOBEL"); return e && *e == '1'; }();
+        if (!via_sobel) return (int)launch_pack_f_batch(n, chw, out, shape, dtype_in, (hipStream_t)hip_stream);
+    }
     for (int i = 0; i < n; ++i) {
         const int *sh = shape + 4 * i;
         const hipError_t e = launch_pack(chw[i], nullptr, nullptr, dtype_in, sh[0], sh[1], sh[2], out[i], dtype_out,

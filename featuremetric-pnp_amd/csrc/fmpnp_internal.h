@@ -52,6 +52,9 @@ hipError_t launch_pack(const void *chw, const void *gx, const void *gy, int dtyp
                        int dtype_out, int cs, int normalized, int replicate, hipStream_t stream, int planes = 3);
 hipError_t launch_gather_ref(const void *ref, int dtype_in, int C, int H, int W, const double *inl, int N, int img0,
                              int img1, void *out, int dtype_out, int ld_out, int *err, hipStream_t stream);
+// n f-only packs (FMPNP_LAYOUT_F, fp32 out) in ceil(n / 32) launches; shape[4i..] = C, H, W, cstride
+hipError_t launch_pack_f_batch(int n, const void *const *chw, void *const *out, const int *shape, int dtype_in,
+                               hipStream_t stream);
 // n gathers in ceil(n / 32) launches (item table in the kernel arguments); err: [n] device flags
 hipError_t launch_gather_ref_batch(int n, const void *const *ref, const int *ref_shape, const double *const *inl,
                                    const int *n_inl, int img0, int img1, void *const *out, const int *ld_out,

@@ -423,11 +423,9 @@ static hipError_t pack_t(const void *chw, const void *gx, const void *gy, int C,
 constexpr int HC_NT = 256;
 
 template <typename Tin, int HC_CT, int HC_XT>
-__global__ __launch_bounds__(HC_NT) void hwc_kernel(const Tin *__restrict__ chw, int C, int H, int W,
-                                                  float *__restrict__ out, int cs, int nct, int nxt, int vec_ok) {
+__device__ __forceinline__ void hwc_tile(const Tin *__restrict__ chw, int C, int H, int W, float *__restrict__ out,
+                                         int cs, int nct, int nxt, int vec_ok, int b, float *tile) {
     constexpr int HC_LD = HC_XT + 1;  // odd row stride of the [channel][column] LDS tile
-    __shared__ float tile[HC_CT * HC_LD];
-    int b = blockIdx.x;
     const int ct = b % nct;
     b /= nct;
     const int xt = b % nxt, y = b / nxt;
@@ -475,6 +473,39 @@ __global__ __launch_bounds__(HC_NT) void hwc_kernel(const Tin *__restrict__ chw,
     }
 }
 
+template <typename Tin, int HC_CT, int HC_XT>
+__global__ __launch_bounds__(HC_NT) void hwc_kernel(const Tin *__restrict__ chw, int C, int H, int W,
+                                                  float *__restrict__ out, int cs, int nct, int nxt, int vec_ok) {
+    __shared__ float tile[HC_CT * (HC_XT + 1)];
+    hwc_tile<Tin, HC_CT, HC_XT>(chw, C, H, W, out, cs, nct, nxt, vec_ok, blockIdx.x, tile);
+}
+
+// Many maps in one launch (fmpnp_pack_features_batch, FMPNP_LAYOUT_F): the item table in the
+// kernel arguments, workgroup b takes tile b - start[i] of the item i whose range holds b --
+// one grid for the batch instead of one ramp-up and tail per map.
+constexpr int HB_MAX = 32;
+struct HwcItems {
+    const void *chw[HB_MAX];
+    float *out[HB_MAX];
+    int C[HB_MAX], H[HB_MAX], W[HB_MAX], cs[HB_MAX], nct[HB_MAX], nxt[HB_MAX], vec[HB_MAX];
+    int start[HB_MAX + 1];
+    int n;
+};
+
+template <typename Tin, int HC_CT, int HC_XT>
+__global__ __launch_bounds__(HC_NT) void hwc_batch_kernel(HwcItems it) {
+    __shared__ float tile[HC_CT * (HC_XT + 1)];
+    const int b = blockIdx.x;
+    int lo = 0, hi = it.n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (it.start[mid] <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    hwc_tile<Tin, HC_CT, HC_XT>(reinterpret_cast<const Tin *>(it.chw[lo]), it.C[lo], it.H[lo], it.W[lo], it.out[lo],
+                                it.cs[lo], it.nct[lo], it.nxt[lo], it.vec[lo], b - it.start[lo], tile);
+}
+
 template <typename Tin, int CT, int XT>
 static hipError_t hwc_ct(const void *chw, int C, int H, int W, void *out, int cs, hipStream_t stream) {
     const int nct = (cs + CT - 1) / CT, nxt = (W + XT - 1) / XT;
@@ -494,6 +525,43 @@ static hipError_t hwc_t(const void *chw, int C, int H, int W, void *out, int cs,
                                    : hwc_ct<Tin, 64, 64>(chw, C, H, W, out, cs, stream);
     if (ct == 128) return hwc_ct<Tin, 128, 32>(chw, C, H, W, out, cs, stream);
     return hwc_ct<Tin, 64, 32>(chw, C, H, W, out, cs, stream);
+}
+
+template <typename Tin>
+static hipError_t hwc_batch_t(const HwcItems &it, int total, hipStream_t stream) {
+    hipLaunchKernelGGL((hwc_batch_kernel<Tin, 64, 32>), dim3((unsigned)total), dim3(HC_NT), 0, stream, it);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_f_batch(int n, const void *const *chw, void *const *out, const int *shape, int dtype_in,
+                               hipStream_t stream) {
+    constexpr int CT = 64, XT = 32;  // the single-map default (hwc_t)
+    for (int i0 = 0; i0 < n; i0 += HB_MAX) {
+        HwcItems it{};
+        const int m = n - i0 < HB_MAX ? n - i0 : HB_MAX;
+        long total = 0;
+        for (int j = 0; j < m; ++j) {
+            const int *sh = shape + 4 * (i0 + j);
+            const int C = sh[0], H = sh[1], W = sh[2], cs = sh[3];
+            if (cs % 4 != 0 || ((uintptr_t)out[i0 + j] % 16) != 0) return hipErrorInvalidValue;
+            it.chw[j] = chw[i0 + j];
+            it.out[j] = reinterpret_cast<float *>(out[i0 + j]);
+            it.C[j] = C; it.H[j] = H; it.W[j] = W; it.cs[j] = cs;
+            it.nct[j] = (cs + CT - 1) / CT;
+            it.nxt[j] = (W + XT - 1) / XT;
+            const size_t es = dtype_in == FMPNP_F64 ? 8 : 4;
+            it.vec[j] = ((uintptr_t)chw[i0 + j] % 16 == 0) && ((size_t)W * es) % 16 == 0;
+            it.start[j] = (int)total;
+            total += (long)it.nct[j] * it.nxt[j] * H;
+            if (total >= (1L << 31)) return hipErrorInvalidValue;
+        }
+        it.start[m] = (int)total;
+        it.n = m;
+        const hipError_t e = dtype_in == FMPNP_F32 ? hwc_batch_t<float>(it, (int)total, stream)
+                                                   : hwc_batch_t<double>(it, (int)total, stream);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_pack(const void *chw, const void *gx, const void *gy, int dtype_in, int C, int H, int W, void *out,

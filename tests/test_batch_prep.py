@@ -90,3 +90,27 @@ def test_batched_gather_with_empty_items_and_more_than_one_launch():
         one = rf.gather_reference(refs[i], inls[i].cpu().numpy(), (48, 48), cstride=16)
         assert torch.equal(one, outs[i])
 
+
+
+def test_batched_f_only_pack_equals_single_calls():
+    """FMPNP_LAYOUT_F batch (one launch per 32 maps) against single-map f-only packs, on
+    mixed shapes (padded channel counts zero-filled) across two launches."""
+    import torch
+    from fmpnp import _lib, refine as rf
+    dev = torch.device("cuda", 0)
+    L = _lib.load()
+    vp = ctypes.c_void_p
+    g = torch.Generator().manual_seed(12)
+    shapes = [(37, 20, 28), (64, 33, 40), (5, 9, 13), (256, 24, 32)] * 9   # 36 maps
+    maps = [torch.randn(s, generator=g).to(dev) for s in shapes]
+    single = [rf.pack_features(m, storage=torch.float32, device=dev, layout="f").buf for m in maps]
+    outs = [torch.full_like(b, 7.0) for b in single]   # padding must be overwritten with zeros
+    n = len(maps)
+    shape_arr = (ctypes.c_int * (4 * n))(*[v for (C, H, W), b in zip(shapes, single) for v in (C, H, W, b.shape[2])])
+    rc = L.fmpnp_pack_features_batch(n, (vp * n)(*[m.data_ptr() for m in maps]),
+                                     (vp * n)(*[o.data_ptr() for o in outs]), shape_arr, _lib.F32, _lib.F32, 0, 0,
+                                     _lib.LAYOUT_F, _lib.stream_ptr(dev))
+    _lib.check(rc, "pack batch f")
+    torch.cuda.synchronize()
+    for a, b in zip(single, outs):
+        assert torch.equal(a, b)
