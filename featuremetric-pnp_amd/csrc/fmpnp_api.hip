@@ -221,6 +221,20 @@ int fmpnp_gather_reference(const void *ref_chw, int dtype_in, int C, int H_ref, 
     return herr ? FMPNP_EINVAL : 0;  // an inlier outside the reference map (reference: IndexError)
 }
 
+int fmpnp_point_costs(const fmpnp_problem *prob, int layout, int dtype, double *cost, int *supported,
+                      void *hip_stream) {
+    if (!prob || !cost || !supported) return FMPNP_EINVAL;
+    const fmpnp_problem &p = *prob;
+    if (p.N == 0) return 0;
+    if (p.N < 0 || !p.feat || !p.fref || !p.pts3d || p.Hf <= 0 || p.Wf <= 0 || p.im_width <= 0 || p.im_height <= 0)
+        return FMPNP_EINVAL;
+    if (p.c_begin < 0 || p.c_end <= p.c_begin || p.c_end > p.cstride || p.ld_ref < p.c_end) return FMPNP_EINVAL;
+    if (layout != FMPNP_LAYOUT_FGRAD && layout != FMPNP_LAYOUT_F) return FMPNP_EINVAL;
+    if (dtype != FMPNP_F32 && dtype != FMPNP_F64) return FMPNP_EINVAL;
+    if (layout == FMPNP_LAYOUT_F && dtype != FMPNP_F32) return FMPNP_EINVAL;
+    return (int)launch_point_costs(p, layout, dtype, cost, supported, (hipStream_t)hip_stream);
+}
+
 int fmpnp_pack_features_f(const void *chw, int dtype_in, int C, int H, int W, void *out, int dtype_out,
                           int cstride, void *hip_stream) {
     if (!chw || !out || C <= 0 || H <= 0 || W <= 0 || cstride < C || cstride % 4) return FMPNP_EINVAL;

@@ -60,4 +60,8 @@ hipError_t launch_gather_ref_batch(int n, const void *const *ref, const int *ref
                                    const int *n_inl, int img0, int img1, void *const *out, const int *ld_out,
                                    int dtype_in, int dtype_out, int *err, hipStream_t stream);
 
+// per-point 0.5 ||f(p_i) - fref_i||^2 and support at the descriptor's pose (fmpnp_point_costs)
+hipError_t launch_point_costs(const fmpnp_problem &p, int layout, int dtype, double *cost, int *supported,
+                              hipStream_t stream);
+
 }  // namespace fmpnp

@@ -91,6 +91,8 @@ def load():
     L.fmpnp_pack_features_batch.restype = i
     L.fmpnp_gather_reference_batch.argtypes = [i, vp, vp, vp, vp, i, i, vp, vp, i, i, vp, vp]
     L.fmpnp_gather_reference_batch.restype = i
+    L.fmpnp_point_costs.argtypes = [ctypes.POINTER(Problem), i, i, vp, vp, vp]
+    L.fmpnp_point_costs.restype = i
     L.fmpnp_workspace_size.argtypes = [ctypes.POINTER(Problem), i, ctypes.POINTER(Options)]
     L.fmpnp_workspace_size.restype = ctypes.c_size_t
     L.fmpnp_refine_batch_async.argtypes = [vp, ctypes.POINTER(Problem), i, i, ctypes.POINTER(Options), vp, vp, i, vp,

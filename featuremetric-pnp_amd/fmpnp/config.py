@@ -8,12 +8,22 @@ from . import losses
 _MODEL = dict(n_iters=50, loss_fn=losses.squared_loss, lambda_=0.01, verbose=False, ratio_threshold=None,
               useGPU=True)  # featurePnP/model.gin:1-5
 _ADAPTER = dict(image_shape=(1024, 1024), feature_pyramid=None)
+# find_inliers.* (featurePnP/model.py:131; input_configs/robotcar_inlier_GN.gin:42 binds 0.8)
+_FIND_INLIERS = dict(threshold=None, loss_fn=losses.squared_loss, mode="ratio_max")
 
 
 def configure(**kwargs):
-    """configure(n_iters=50, loss_fn=..., ratio_threshold=..., image_shape=..., feature_pyramid=...)."""
+    """configure(n_iters=50, loss_fn=..., ratio_threshold=..., image_shape=..., feature_pyramid=...,
+    find_inliers_threshold=..., find_inliers_loss_fn=..., find_inliers_mode=...)."""
     for k, v in kwargs.items():
-        if k in _ADAPTER:
+        if k.startswith("find_inliers_"):
+            k = k[len("find_inliers_"):]
+            if k not in _FIND_INLIERS:
+                raise KeyError(f"find_inliers has no parameter {k!r}")
+            if isinstance(v, str) and k == "loss_fn":
+                v = losses.BY_NAME[v]
+            _FIND_INLIERS[k] = v
+        elif k in _ADAPTER:
             _ADAPTER[k] = v
         else:
             if isinstance(v, str) and k == "loss_fn":
@@ -27,3 +37,7 @@ def model_kwargs():
 
 def adapter_kwargs():
     return dict(_ADAPTER)
+
+
+def find_inliers_kwargs():
+    return dict(_FIND_INLIERS)

@@ -18,6 +18,7 @@ import torch
 from torch import nn
 
 from . import _lib
+from . import config as _config
 from . import losses as _losses
 from . import refine as _rf
 
@@ -180,6 +181,51 @@ class sparseFeaturePnP(nn.Module):
             lf = _rf.pack_features(lvl[0], storage=feats.dtype, device=feats.buf.device)
             R, t = self._forward_packed(lf, pts3D, fref_t[:, start:end_c], K, im_width, im_height, R, t, track)
         return R, t
+
+
+def find_inliers(pts3D, R, t, feature_map_query, feature_ref, K, im_width, im_height, threshold=None, loss_fn=None,
+                 mode=None, storage=None, device=None):
+    """featurePnP/model.py:131-152 on the device: a bool mask [N] (CPU) of the points whose
+    rounded projection at (R, t) lies in the image and whose loss of 0.5||f(p) - fref||^2
+    passes the ratio test |rho| < max|rho| * threshold (ratio_threshold_feature_errors,
+    model.py:120-129).  Projection, support and the per-point costs run in one HIP launch
+    (fmpnp_point_costs); loss and ratio mask are N-element device tensor ops.
+
+    threshold / loss_fn / mode default to the gin-style bindings of fmpnp.config
+    (`configure(find_inliers_threshold=0.8)`; the reference's gin binds them).  Like the
+    reference, a mode other than "ratio_max" returns None, a missing threshold raises
+    TypeError, and an empty support set raises (torch.max of an empty tensor)."""
+    fm = feature_map_query if isinstance(feature_map_query, torch.Tensor) else torch.as_tensor(
+        np.asarray(feature_map_query))
+    if fm.dim() == 4:
+        fm = fm[0]
+    if device is None:
+        device = fm.device if fm.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    storage = storage or (torch.float64 if fm.dtype == torch.float64 else torch.float32)
+    feats = _rf.pack_features(fm, storage=storage, device=device, layout="f" if storage == torch.float32 else "fgrad")
+    return _find_inliers_packed(feats, pts3D, R, t, feature_ref, K, im_width, im_height, threshold, loss_fn, mode)
+
+
+def _find_inliers_packed(feats, pts3D, R, t, feature_ref, K, im_width, im_height, threshold=None, loss_fn=None,
+                         mode=None):
+    cfg = _config.find_inliers_kwargs()
+    threshold = cfg["threshold"] if threshold is None else threshold
+    loss_fn = cfg["loss_fn"] if loss_fn is None else loss_fn
+    mode = cfg["mode"] if mode is None else mode
+    pts = pts3D if isinstance(pts3D, torch.Tensor) else np.asarray(pts3D, dtype=np.float64)
+    prob = _rf.make_problem(feats, feature_ref, pts, _to_np(K, (3, 3)), im_width, im_height, _to_np(R, (3, 3)),
+                            _to_np(t, (3,)))
+    cost, sup = _rf.point_costs(prob)                                           # model.py:133-146
+    if mode != "ratio_max":                                                     # model.py:149 (no else)
+        return None
+    if threshold is None:
+        raise TypeError("find_inliers needs a threshold (the reference's gin binds find_inliers.threshold, "
+                        "model.py:131; fmpnp.config.configure(find_inliers_threshold=...))")
+    rho = loss_fn(cost[sup])[0]                                                 # model.py:147
+    limit = torch.max(torch.abs(rho)) * threshold                               # model.py:122
+    mask = sup.clone()
+    mask[sup] = torch.abs(rho) < limit                                          # model.py:123,151
+    return mask.cpu()
 
 
 def _gaussian_blur(x, kernel_size, sigma=1.0):

@@ -13,13 +13,46 @@ import torch
 from . import config
 from . import refine as _rf
 from .matrix_utils import matrix_quaternion
-from .model import sparseFeaturePnP
+from .model import _find_inliers_packed, sparseFeaturePnP
 
 
 def _new_model(model):
     if model is not None:
         return model
     return sparseFeaturePnP(**config.model_kwargs())  # "Parameters from gin!" (optimize_feature_pnp.py:63)
+
+
+def feature_pnp_multi(query_hypercolumns, reference_hypercolumns, prediction, K, image_shape, track=False,
+                      model=None, storage=None, rounds=3):
+    """optimize_feature_pnp.py:20-47: refine on the current inliers, re-select the inliers
+    with find_inliers at the new pose, three times.  The initial inliers are
+    prediction.inlier_mask, or find_inliers at the initial pose when it is None.  The query
+    map is packed once (f-only layout for fp32 texels); every round reuses it and the
+    device fref.  Returns (R, t, model) like feature_pnp."""
+    model = _new_model(model)
+    q = query_hypercolumns[0] if query_hypercolumns.dim() == 4 else query_hypercolumns
+    dev = q.device if q.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    storage = storage or model.storage or (torch.float64 if q.dtype == torch.float64 else torch.float32)
+    layout = "f" if storage == torch.float32 and getattr(model, "sampling", "nearest") == "nearest" else "fgrad"
+    feats = _rf.pack_features(q, storage=storage, device=dev, layout=layout)               # :28,31
+    fref = _rf.gather_reference(reference_hypercolumns, prediction.reference_inliers, image_shape,
+                                cstride=feats.cstride, storage=storage, device=dev)          # :21-26
+    pts3D = np.asarray(prediction.points_3d, dtype=np.float64).reshape(-1, 3)               # :22
+    T = np.asarray(prediction.matrix, dtype=np.float64)
+    R, t = torch.from_numpy(T[:3, :3].copy()), torch.from_numpy(T[:3, 3].copy())             # :30-31
+    Kt = K if isinstance(K, torch.Tensor) else torch.from_numpy(np.asarray(K, dtype=np.float64))
+    W, H = image_shape[0], image_shape[1]
+    if prediction.inlier_mask is not None:                                                  # :35-39
+        inliers = torch.zeros(pts3D.shape[0], dtype=torch.bool)
+        inliers[torch.as_tensor(np.asarray(prediction.inlier_mask))] = True
+    else:
+        print("No initial inliers found.")
+        inliers = _find_inliers_packed(feats, pts3D, R, t, fref, Kt, W, H)
+    for _ in range(rounds):                                                                 # :43-46
+        idx = inliers.numpy()
+        R, t = model._forward_packed(feats, pts3D[idx], fref[inliers.to(dev)], Kt, W, H, R, t, track)
+        inliers = _find_inliers_packed(feats, pts3D, R, t, fref, Kt, W, H)
+    return R, t, model
 
 
 def feature_pnp(query_hypercolumns, reference_hypercolumns, prediction, K, image_shape, track=False,
@@ -85,6 +118,11 @@ class DirectPoseModel:
         kw = dict(config.model_kwargs())
         kw.update(self.model_kwargs)
         return sparseFeaturePnP(**kw)
+
+    def feature_pnp_multi(self, query_hypercolumns, reference_hypercolumns, prediction, K, image_shape,
+                          track=False):
+        return feature_pnp_multi(query_hypercolumns, reference_hypercolumns, prediction, K, image_shape, track,
+                                 model=self.make_model())
 
     def feature_pnp(self, query_hypercolumns, reference_hypercolumns, prediction, K, image_shape, track=False,
                     feature_pyramid=None):

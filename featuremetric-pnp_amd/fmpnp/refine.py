@@ -392,6 +392,29 @@ class AsyncBatch:
         return results_from_array(self.d_res.cpu().numpy().view(RESULT_DTYPE))
 
 
+def point_costs(problem, R=None, t=None):
+    """Per-point 0.5 ||f(p_i) - fref_i||^2 and support at (R, t) (default: the problem's
+    R0, t0) on the device -- the projection, points_within_image and indexing_ of
+    find_inliers (featurePnP/model.py:132-146), fmpnp_point_costs.  Returns device tensors
+    (cost [N] fp64, 0 where unsupported; supported [N] bool)."""
+    p = problem.descriptor()
+    if R is not None:
+        p.R0[:] = list(_mat(R, 9))
+    if t is not None:
+        p.t0[:] = list(_mat(t, 3))
+    dev = problem.feats.buf.device
+    N = int(p.N)
+    cost = torch.zeros(N, dtype=torch.float64, device=dev)
+    sup = torch.zeros(N, dtype=torch.int32, device=dev)
+    lay = _lib.LAYOUT_F if problem.feats.layout == "f" else _lib.LAYOUT_FGRAD
+    with torch.cuda.device(dev):
+        rc = _lib.load().fmpnp_point_costs(ctypes.byref(p), lay, problem.feats.dtype_code,
+                                           ctypes.c_void_p(cost.data_ptr()), ctypes.c_void_p(sup.data_ptr()),
+                                           _lib.stream_ptr(dev))
+    _lib.check(rc, "fmpnp_point_costs")
+    return cost, sup.bool()
+
+
 def project_pixels(R, t, pts3d, K):
     """Host restatement of the pixel projection (model.py:303-308) for track_['points2d'];
     elementwise numpy (no FMA), matching the device's sequential fp64 arithmetic."""

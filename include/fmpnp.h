@@ -19,6 +19,10 @@
  *   fmpnp_gather_reference
  *   fmpnp_gather_reference_async / fmpnp_gather_reference_batch
  *       replaces the per-point fref gather       optimize_feature_pnp.py:51-56.
+ *   fmpnp_point_costs
+ *       replaces find_inliers' per-point costs   featurePnP/model.py:132-146
+ *       (projection, support mask, indexing_, 0.5||e||^2; the loss and ratio mask,
+ *        model.py:147-152, stay in the façade).
  *
  * Conventions: plain pointers and sizes, no torch types.  Feature / point
  * buffers are caller-owned DEVICE memory; results and traces of the
@@ -181,6 +185,16 @@ int fmpnp_gather_reference_batch(int n, const void *const *ref_chw, const int *r
                                  const double *const *ref_inliers, const int *n_inliers, int img0, int img1,
                                  void *const *out, const int *ld_out, int dtype_in, int dtype_out, int *err_flags,
                                  void *hip_stream);
+
+/* Per-point residual costs at the descriptor's pose (R0, t0): the projection,
+ * points_within_image and indexing_ of find_inliers (featurePnP/model.py:132-146).
+ * supported[i] = 1 when point i's rounded pixel lies in the image, and then
+ * cost[i] = 0.5 * sum over [c_begin, c_end) of (f(p_i) - fref_i)^2 (fp64), else 0.
+ * cost ([N] fp64) and supported ([N] int32) are DEVICE arrays; the descriptor is host
+ * memory; asynchronous on hip_stream.  layout / dtype as in fmpnp_options (FMPNP_LAYOUT_F
+ * is fp32 only).  The façade's find_inliers applies the loss and the ratio mask. */
+int fmpnp_point_costs(const fmpnp_problem *prob, int layout, int dtype, double *cost, int *supported,
+                      void *hip_stream);
 
 /* Device workspace needed by fmpnp_refine_batch_async for n problems. */
 size_t fmpnp_workspace_size(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt);

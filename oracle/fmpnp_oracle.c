@@ -504,6 +504,47 @@ double orc_compute_cost(const orc_problem *pb, double ratio_threshold, const dou
     return eo.n_supported == 0 ? NAN : eo.cost_mean;
 }
 
+/* find_inliers (model.py:132-152, mode "ratio_max"): project at (R, t), support mask
+ * (points_within_image), NN gather (indexing_), cost = 0.5 ||e||^2, (rho, .) = loss(cost),
+ * then ratio_threshold_feature_errors (model.py:120-129) over the supported points:
+ * mask[n] = supported and |rho_n| < max |rho| * threshold.  cost_out[n] = 0.5 ||e||^2
+ * (0 if unsupported).  Returns the number of supported points (0: the reference's
+ * torch.max of an empty tensor raises). */
+int orc_find_inliers(const orc_problem *pb, const double R[9], const double t[3], int loss, double alpha,
+                     double threshold, unsigned char *mask, double *cost_out)
+{
+    const int N = pb->N, C = pb->C;
+    const long plane = (long)pb->Hf * pb->Wf;
+    double *rho = (double *)malloc(sizeof(double) * (N > 0 ? N : 1));
+    int nsup = 0;
+    double rmax = 0.0;
+    for (int n = 0; n < N; ++n) {
+        double P[3], qx, qy, d1;
+        long x, y;
+        transform(R, t, pb->pts + 3 * n, P);
+        mask[n] = (unsigned char)project(pb->K, P, pb->im_w, pb->im_h, &x, &y, &qx, &qy);
+        cost_out[n] = 0.0;
+        if (!mask[n]) continue;
+        const long off = ((y * (long)pb->Hf) / pb->im_h) * pb->Wf + (x * (long)pb->Wf) / pb->im_w;
+        const double *fr = pb->fref + (long)n * pb->ld_ref;
+        double s = 0.0;
+        for (int c = 0; c < C; ++c) {
+            const double e = pb->fmap[c * plane + off] - fr[c];
+            s += e * e;
+        }
+        cost_out[n] = 0.5 * s;
+        loss_eval(loss, alpha, cost_out[n], &rho[n], &d1);
+        const double a = fabs(rho[n]);
+        if (nsup == 0 || a > rmax || isnan(a)) rmax = isnan(rmax) ? rmax : a;
+        nsup++;
+    }
+    const double limit = rmax * threshold;
+    for (int n = 0; n < N; ++n)
+        if (mask[n]) mask[n] = (unsigned char)(fabs(rho[n]) < limit);
+    free(rho);
+    return nsup;
+}
+
 /* Sobel (helpers/sobel_pytorch.py:9-59 via utils.py:81-104): cross-correlation
  * with kx = [[-1,0,1],[-2,0,2],[-1,0,1]], ky = kx^T, zero padding, unnormalised. */
 void orc_sobel(const double *x, int C, int H, int W, double *gx, double *gy)

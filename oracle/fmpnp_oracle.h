@@ -46,6 +46,8 @@ typedef struct { /* optional per-eval / per-step trace, capacity cap entries eac
 
 int orc_forward(const orc_problem *pb, const orc_options *op, orc_result *res, orc_trace *tr);
 double orc_compute_cost(const orc_problem *pb, double ratio_threshold, const double R[9], const double t[3]);
+int orc_find_inliers(const orc_problem *pb, const double R[9], const double t[3], int loss, double alpha,
+                     double threshold, unsigned char *mask, double *cost_out);
 void orc_sobel(const double *x, int C, int H, int W, double *gx, double *gy);
 int orc_forward_batch(const orc_problem *pbs, int n, const orc_options *op, orc_result *res, int nthreads);
 

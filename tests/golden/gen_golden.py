@@ -488,5 +488,90 @@ def gen_adapter():
     np.savez_compressed(os.path.join(HERE, "quaternion.npz"), M=np.stack(Ms), q=np.stack(Qs))
 
 
+def gen_find_inliers():
+    """find_inliers (model.py:131-152) on the shared C=16 scene, and feature_pnp_multi
+    (optimize_feature_pnp.py:20-47) on the adapter maps with and without initial inliers.
+    find_inliers.threshold = 0.8 is input_configs/robotcar_inlier_GN.gin:42's binding."""
+    import functools
+    import pose_prediction.optimize_feature_pnp as ofp
+
+    def find_inliers_ref(pts3D, R, t, feature_map_query, feature_ref, K, im_width, im_height, threshold=None,
+                         loss_fn=refutils.squared_loss, mode="ratio_max"):
+        # model.py:132-152 line for line, from the reference's own functions.  The reference
+        # body itself raises under torch 2.10 at :151 (`mask_supported[mask_supported] = ...`
+        # writes through its own index: "some elements ... refer to a single memory
+        # location"); the index is cloned here, which is what older torch did implicitly.
+        points_3d = torch.mm(R, pts3D.T).T + t
+        points_2d = torch.round(refutils.from_homogeneous(torch.mm(K, points_3d.T).T)).type(torch.IntTensor) - 1
+        mask_supported = refmodel.points_within_image(points_2d, im_width, im_height)
+        points_2d_supported = points_2d[mask_supported, :]
+        error = refmodel.indexing_(feature_map_query, torch.flip(points_2d_supported, (1,)), im_width,
+                                   im_height) - feature_ref[mask_supported]
+        cost = 0.5 * (error ** 2).sum(-1)
+        cost_full, weights, _ = loss_fn(cost)
+        if mode == "ratio_max":
+            threshold_mask = refmodel.ratio_threshold_feature_errors(cost_full, threshold=threshold)
+            mask_supported[mask_supported.clone()] = threshold_mask
+            return mask_supported
+
+    rng, f32, K, pts, W, H = shared_scene()
+    fm = f32.double()
+    R0 = rot_xyz(0.6, -0.4, 2.0)
+    t0 = np.array([0.20, -0.12, 0.35])
+    fref = fref_identity(fm, pts, K, W, H).numpy()
+    poses = {"init": (R0, t0), "ident": (np.eye(3), np.zeros(3)), "shift": (np.eye(3), np.array([2.5, 0.0, 0.0]))}
+    out = {}
+    for tag, (R, t) in poses.items():
+        for loss in ("squared", "geman_mcclure", "cauchy"):
+            for thr in (0.8, 0.5):
+                m = find_inliers_ref(torch.from_numpy(pts), torch.from_numpy(R), torch.from_numpy(t), fm,
+                                     torch.from_numpy(fref), torch.from_numpy(K), W, H, threshold=thr,
+                                     loss_fn=loss_fn_for(loss))
+                out[f"mask_{tag}_{loss}_{thr}"] = m.numpy().astype(np.int8)
+    np.savez_compressed(os.path.join(HERE, "find_inliers.npz"), in_pts3d=pts, in_fref=fref, in_K=K, in_im_width=W,
+                        in_im_height=H, **{f"in_R_{k}": v[0] for k, v in poses.items()},
+                        **{f"in_t_{k}": v[1] for k, v in poses.items()},
+                        meta=np.array(json.dumps({"shared_fmap": "fmap_c16", "poses": list(poses)})), **out)
+    print("find_inliers:", {k: int(v.sum()) for k, v in out.items() if "0.8" in k})
+
+    Prediction = namedtuple("Prediction", "success num_matches num_inliers reference_inliers query_inliers "
+                            "points_3d quaternion matrix reference_filename reference_keypoints inlier_mask")
+    rng = np.random.Generator(np.random.PCG64(31))
+    C, Hh, Wh = 8, 44, 44
+    q32 = make_fmap(rng, C, Hh, Wh)
+    r32 = make_fmap(rng, C, Hh, Wh)
+    image_shape = (192, 192)
+    Kc = make_K(*image_shape)
+    N = 60
+    pts = make_points(rng, N, Kc, *image_shape)
+    ref_inl = np.stack([rng.uniform(0, image_shape[0] - 0.01, N), rng.uniform(0, image_shape[1] - 0.01, N)], 1)
+    T = np.eye(4)
+    T[:3, :3] = rot_xyz(0.4, -0.2, 1.0)
+    T[:3, 3] = [0.08, -0.04, 0.15]
+    ofp.sparseFeaturePnP = functools.partial(refmodel.sparseFeaturePnP, n_iters=10,
+                                             loss_fn=refutils.geman_mcclure_loss, lambda_=0.01)
+    ofp.find_inliers = functools.partial(find_inliers_ref, threshold=0.8)
+    res = {}
+    for tag, inl in (("none", None), ("given", np.arange(0, N, 2))):
+        pred = Prediction(True, N, N, ref_inl, None, pts.reshape(N, 1, 3), None, T, "ref.png", None, inl)
+        R, t, mdl = ofp.feature_pnp_multi(q32[None], r32[None], pred, torch.from_numpy(Kc), image_shape)
+        res[f"out_R_{tag}"] = R.numpy()
+        res[f"out_t_{tag}"] = t.numpy()
+        res[f"initial_cost_{tag}"] = np.array(float(mdl.initial_cost_))
+        res[f"best_cost_{tag}"] = np.array(float(mdl.best_cost_))
+        res[f"best_num_inliers_{tag}"] = np.array(int(mdl.best_num_inliers_))
+        print(f"feature_pnp_multi/{tag}: best={float(mdl.best_cost_):.6g} inliers={int(mdl.best_num_inliers_)}")
+    np.savez_compressed(os.path.join(HERE, "feature_pnp_multi.npz"), in_query=q32.numpy(), in_ref=r32.numpy(),
+                        in_points_3d=pts.reshape(N, 1, 3), in_reference_inliers=ref_inl, in_matrix=T, in_K=Kc,
+                        in_mask_given=np.arange(0, N, 2),
+                        meta=np.array(json.dumps(dict(n_iters=10, lambda0=0.01, loss="geman_mcclure",
+                                                      find_inliers_threshold=0.8, image_shape=list(image_shape)))),
+                        **res)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["find_inliers"]:  # only the find_inliers / feature_pnp_multi fixtures
+        gen_find_inliers()
+    else:
+        main()
+        gen_find_inliers()

@@ -96,6 +96,19 @@ def test_entry_points_reject_bad_arguments_without_a_device():
     o.sampling, o.layout = _lib.NEAREST, 5
     assert L.fmpnp_refine_batch(ctypes.byref(pb), 1, ctypes.byref(o), ctypes.byref(res), None, 0, None) == -1
     assert L.fmpnp_gather_reference_batch(1, None, None, None, None, 1, 1, None, None, 0, 0, None, None) == -1
+    # per-point costs: missing outputs, a bad channel range or layout are refused
+    vpp = ctypes.c_void_p
+    assert L.fmpnp_point_costs(None, 0, 0, None, None, None) == -1
+    p = _lib.Problem()
+    p.N, p.feat, p.fref, p.pts3d = 4, 16, 16, 16
+    p.Hf = p.Wf = p.im_width = p.im_height = 8
+    p.cstride, p.c_begin, p.c_end, p.ld_ref = 4, 0, 8, 8           # c_end > cstride
+    assert L.fmpnp_point_costs(ctypes.byref(p), 0, 0, vpp(16), vpp(16), None) == -1
+    p.c_end = 4
+    assert L.fmpnp_point_costs(ctypes.byref(p), 3, 0, vpp(16), vpp(16), None) == -1  # unknown layout
+    assert L.fmpnp_point_costs(ctypes.byref(p), _lib.LAYOUT_F, _lib.F64, vpp(16), vpp(16), None) == -1
+    p.N = 0
+    assert L.fmpnp_point_costs(ctypes.byref(p), 0, 0, vpp(16), vpp(16), None) == 0
     rshape = (ctypes.c_int * 6)(4, 2, 2, 4, 2, 2)
     n_in = (ctypes.c_int * 2)(3, -1)                    # item 1: negative point count
     ld = (ctypes.c_int * 2)(4, 4)

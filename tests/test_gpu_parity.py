@@ -404,3 +404,89 @@ def test_async_batch_matches_sync():
     ab.launch()
     for r in ab.results():
         assert np.array_equal(r["R"], sync_r["R"]) and np.array_equal(r["t"], sync_r["t"])
+
+
+@pytest.mark.parametrize("storage", [torch.float64, torch.float32])
+def test_find_inliers_matches_reference(storage):
+    """find_inliers (model.py:131-152) through fmpnp_point_costs: the reference's masks for
+    every pose / loss / threshold of the fixture; per-point costs against the oracle's to
+    1e-12 relative (summation order).  The C=16 map is fp32 data, so fp32 (f-only layout)
+    and fp64 storage hold the same values and give the same masks."""
+    z = load_npz("find_inliers")
+    f = shared_fmap("fmap_c16").astype(np.float64)
+    fm = torch.from_numpy(f).to(storage)
+    W, H = int(z["in_im_width"]), int(z["in_im_height"])
+    losses = {"squared": fmpnp.squared_loss, "geman_mcclure": fmpnp.geman_mcclure_loss,
+              "cauchy": fmpnp.cauchy_loss}
+    for tag in ("init", "ident", "shift"):
+        R, t = z[f"in_R_{tag}"], z[f"in_t_{tag}"]
+        for loss, fn in losses.items():
+            for thr in (0.8, 0.5):
+                m = fmpnp.find_inliers(torch.from_numpy(z["in_pts3d"]), torch.from_numpy(R), torch.from_numpy(t), fm,
+                                       torch.from_numpy(z["in_fref"]), torch.from_numpy(z["in_K"]), W, H,
+                                       threshold=thr, loss_fn=fn)
+                assert m.dtype == torch.bool and m.device.type == "cpu"
+                np.testing.assert_array_equal(m.numpy(), z[f"mask_{tag}_{loss}_{thr}"].astype(bool),
+                                              err_msg=f"{tag} {loss} {thr}")
+        feats = rf.pack_features(fm, storage=storage, device=DEV,
+                                 layout="f" if storage == torch.float32 else "fgrad")
+        prob = rf.make_problem(feats, z["in_fref"], z["in_pts3d"], z["in_K"], W, H, R, t)
+        cost, sup = rf.point_costs(prob)
+        _, ocost, nsup = orc.find_inliers(z["in_pts3d"], z["in_fref"], f, z["in_K"], W, H, R, t, 0.8)
+        assert int(sup.sum()) == nsup
+        np.testing.assert_allclose(cost.cpu().numpy(), ocost, rtol=1e-12, atol=0)
+
+
+def test_find_inliers_reference_errors():
+    """mode other than "ratio_max" -> None; no threshold -> TypeError (gin binds it in the
+    reference); no supported point -> torch.max of an empty tensor raises."""
+    z = load_npz("find_inliers")
+    fm = torch.from_numpy(shared_fmap("fmap_c16").astype(np.float64))
+    args = (torch.from_numpy(z["in_pts3d"]), torch.eye(3, dtype=torch.float64), torch.zeros(3, dtype=torch.float64),
+            fm, torch.from_numpy(z["in_fref"]), torch.from_numpy(z["in_K"]), int(z["in_im_width"]),
+            int(z["in_im_height"]))
+    assert fmpnp.find_inliers(*args, threshold=0.8, mode="other") is None
+    with pytest.raises(TypeError):
+        fmpnp.find_inliers(*args)
+    away = list(args)
+    away[2] = torch.tensor([500.0, 0.0, 0.0], dtype=torch.float64)
+    with pytest.raises(RuntimeError):
+        fmpnp.find_inliers(*away, threshold=0.8)
+    fmpnp.config.configure(find_inliers_threshold=0.8)
+    try:
+        assert fmpnp.find_inliers(*args).shape == (z["in_pts3d"].shape[0],)
+    finally:
+        fmpnp.config.configure(find_inliers_threshold=None)
+
+
+@pytest.mark.parametrize("tag", ["none", "given"])
+@pytest.mark.parametrize("storage", [torch.float64, torch.float32])
+def test_feature_pnp_multi_matches_reference(tag, storage):
+    """feature_pnp_multi (optimize_feature_pnp.py:20-47): three refine + find_inliers rounds.
+    fp64 storage: the reference's pose to 1e-9 and its attributes; fp32 (f-only layout, fp64
+    gradients in the LM kernel): pose within the north star's 1e-4 rad / 1e-4 m."""
+    import json
+    from collections import namedtuple
+    z = load_npz("feature_pnp_multi")
+    meta = json.loads(str(z["meta"]))
+    Pred = namedtuple("Prediction", "points_3d reference_inliers matrix inlier_mask")
+    pred = Pred(z["in_points_3d"], z["in_reference_inliers"], z["in_matrix"],
+                z["in_mask_given"] if tag == "given" else None)
+    q = torch.from_numpy(z["in_query"]).to(DEV)[None]
+    r = torch.from_numpy(z["in_ref"]).to(DEV)[None]
+    model = fmpnp.sparseFeaturePnP(meta["n_iters"], loss_fn=fmpnp.geman_mcclure_loss, lambda_=meta["lambda0"],
+                                   storage=storage)
+    fmpnp.config.configure(find_inliers_threshold=meta["find_inliers_threshold"])
+    try:
+        R, t, model = fmpnp.feature_pnp_multi(q, r, pred, z["in_K"], tuple(meta["image_shape"]), model=model)
+    finally:
+        fmpnp.config.configure(find_inliers_threshold=None)
+    if storage == torch.float64:
+        np.testing.assert_allclose(R.numpy(), z[f"out_R_{tag}"], atol=1e-9)
+        np.testing.assert_allclose(t.numpy(), z[f"out_t_{tag}"], atol=1e-9)
+        assert model.initial_cost_.item() == pytest.approx(float(z[f"initial_cost_{tag}"]), rel=1e-10)
+        assert model.best_cost_.item() == pytest.approx(float(z[f"best_cost_{tag}"]), rel=1e-9)
+        assert model.best_num_inliers_ == int(z[f"best_num_inliers_{tag}"])
+    else:
+        assert rot_angle(R.numpy(), z[f"out_R_{tag}"]) < 1e-4
+        assert np.linalg.norm(t.numpy() - z[f"out_t_{tag}"]) < 1e-4

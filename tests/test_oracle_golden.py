@@ -171,3 +171,59 @@ def test_oracle_adapter_matches_golden(name):
     T[3, :3] = t
     np.testing.assert_allclose(orc.matrix_quaternion(T), z["opt_quat"], atol=1e-10)
     np.testing.assert_allclose(t, z["opt_t"], atol=1e-10)
+
+
+FIND_INLIERS_LOSSES = ("squared", "geman_mcclure", "cauchy")
+
+
+def test_oracle_find_inliers_matches_golden():
+    """find_inliers (model.py:131-152): support, NN costs, loss, ratio mask -- every pose,
+    loss and threshold of the fixture, mask for mask."""
+    z = load_npz("find_inliers")
+    f = shared_fmap("fmap_c16").astype(np.float64)
+    for tag in ("init", "ident", "shift"):
+        for loss in FIND_INLIERS_LOSSES:
+            for thr in (0.8, 0.5):
+                mask, cost, nsup = orc.find_inliers(z["in_pts3d"], z["in_fref"], f, z["in_K"], int(z["in_im_width"]),
+                                                    int(z["in_im_height"]), z[f"in_R_{tag}"], z[f"in_t_{tag}"], thr,
+                                                    loss)
+                np.testing.assert_array_equal(mask, z[f"mask_{tag}_{loss}_{thr}"].astype(bool), err_msg=tag + loss)
+                assert nsup > 0
+
+
+def oracle_feature_pnp_multi(z, given):
+    """optimize_feature_pnp.py:20-47 composed from the oracle's pieces (gather, Sobel, LM, find_inliers)."""
+    import json
+    meta = json.loads(str(z["meta"]))
+    img = meta["image_shape"]
+    fref = orc.gather_reference_features(z["in_ref"].astype(np.float64), z["in_reference_inliers"], img)
+    f = z["in_query"].astype(np.float64)
+    gx, gy = orc.sobel(f)
+    pts = z["in_points_3d"].reshape(-1, 3)
+    R, t = z["in_matrix"][:3, :3], z["in_matrix"][:3, 3]
+    thr = meta["find_inliers_threshold"]
+    if given:
+        inl = np.zeros(len(pts), dtype=bool)
+        inl[z["in_mask_given"]] = True
+    else:
+        inl = orc.find_inliers(pts, fref, f, z["in_K"], img[0], img[1], R, t, thr)[0]
+    o = orc.make_options(meta["n_iters"], meta["lambda0"], meta["loss"])
+    initial = None
+    for _ in range(3):
+        p = orc.make_problem(pts[inl], fref[inl], f, gx, gy, z["in_K"], img[0], img[1], R, t)
+        res, _tr = orc.forward(p, o, 0)
+        R, t = res["R"], res["t"]
+        initial = res["initial_cost"] if initial is None else initial
+        inl = orc.find_inliers(pts, fref, f, z["in_K"], img[0], img[1], R, t, thr)[0]
+    return R, t, initial, res
+
+
+@pytest.mark.parametrize("tag", ["none", "given"])
+def test_oracle_feature_pnp_multi_matches_golden(tag):
+    z = load_npz("feature_pnp_multi")
+    R, t, initial, res = oracle_feature_pnp_multi(z, tag == "given")
+    np.testing.assert_allclose(R, z[f"out_R_{tag}"], atol=POSE_ATOL)
+    np.testing.assert_allclose(t, z[f"out_t_{tag}"], atol=POSE_ATOL)
+    assert initial == pytest.approx(float(z[f"initial_cost_{tag}"]), rel=COST_RTOL)
+    assert res["best_cost"] == pytest.approx(float(z[f"best_cost_{tag}"]), rel=COST_RTOL)
+    assert res["best_num_inliers"] == int(z[f"best_num_inliers_{tag}"])
