@@ -117,10 +117,22 @@ class sparseFeaturePnP(nn.Module):
                     p2d = _rf.project_pixels(tr["R"][k], tr["t"][k], pts_np, Kn)
                     mask = (p2d[:, 0] >= 0) & (p2d[:, 1] >= 0) & (p2d[:, 0] < im_width) & (p2d[:, 1] < im_height)
                     self.track(torch.from_numpy(tr["R"][k].copy()), torch.from_numpy(tr["t"][k].copy()),
-                               float(tr["cost"][k]), torch.from_numpy(p2d), torch.from_numpy(mask), None)
+                               float(tr["cost"][k]), torch.from_numpy(p2d), torch.from_numpy(mask),
+                               self._threshold_mask(prob, tr["R"][k], tr["t"][k]))
         if res["status"] & _lib.STATUS_NAN:
             warnings.warn("NaN detected, exit (model.py:411-413)")
         return (torch.from_numpy(res["R"].copy()), torch.from_numpy(res["t"].copy()))
+
+    def _threshold_mask(self, prob, R, t):
+        """track_["threshold_mask"] at (R, t) (model.py:328,452): the ratio test's mask over the
+        supported points, from the device per-point costs; None without the ratio test."""
+        if not self.use_ratio_test_:
+            return None
+        cost, sup = _rf.point_costs(prob, R, t)
+        rho = torch.abs(self.loss_fn(cost[sup])[0])
+        if rho.numel() == 0:
+            return torch.zeros(0, dtype=torch.bool)
+        return (rho < torch.max(rho) * self.ratio_threshold_).cpu()
 
     def compute_cost(self, pts3D, R, t, feature_map_query, feature_ref, K, im_width, im_height):
         """model.py:216-243: mean 0.5||e||^2 (no loss_fn, optional ratio test); None if no support."""

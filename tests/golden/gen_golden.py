@@ -534,6 +534,24 @@ def gen_find_inliers():
                         meta=np.array(json.dumps({"shared_fmap": "fmap_c16", "poses": list(poses)})), **out)
     print("find_inliers:", {k: int(v.sum()) for k, v in out.items() if "0.8" in k})
 
+    # track_["threshold_mask"] (model.py:328,359,452,465) of the ratio-test cases: one mask over the
+    # supported points per tracked evaluation, stored padded to N (-1 = not supported)
+    inp = base_inputs(f32, K, pts, W, H, R0, t0)
+    for name, opts in (("ratio08_gm", dict(n_iters=30, lambda0=0.01, loss="geman_mcclure", ratio_threshold=0.8)),
+                       ("ratio05_sq", dict(n_iters=20, lambda0=0.01, loss="squared", ratio_threshold=0.5))):
+        m = refmodel.sparseFeaturePnP(n_iters=opts["n_iters"], loss_fn=loss_fn_for(opts["loss"]),
+                                      lambda_=opts["lambda0"], ratio_threshold=opts["ratio_threshold"])
+        m(torch.from_numpy(inp["pts3d"]), torch.from_numpy(inp["fref"]), torch.from_numpy(inp["fmap"]),
+          torch.from_numpy(inp["gx"]), torch.from_numpy(inp["gy"]), torch.from_numpy(K), W, H,
+          R_init=torch.from_numpy(R0), t_init=torch.from_numpy(t0), track=True)
+        tm = np.full((len(m.track_["mask"]), len(pts)), -1, dtype=np.int8)
+        for k, (sup, thm) in enumerate(zip(m.track_["mask"], m.track_["threshold_mask"])):
+            tm[k, sup.numpy()] = thm.numpy().astype(np.int8)
+        np.savez_compressed(os.path.join(HERE, f"track_thr_{name}.npz"), threshold_mask=tm,
+                            track_costs=np.array(m.track_["costs"], dtype=np.float64),
+                            meta=np.array(json.dumps({"case": name})))
+        print(f"track_thr_{name}: {tm.shape}, kept per eval {[(r == 1).sum() for r in tm[:4]]}")
+
     Prediction = namedtuple("Prediction", "success num_matches num_inliers reference_inliers query_inliers "
                             "points_3d quaternion matrix reference_filename reference_keypoints inlier_mask")
     rng = np.random.Generator(np.random.PCG64(31))

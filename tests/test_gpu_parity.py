@@ -279,6 +279,12 @@ def test_forward_facade_track_matches_reference():
     np.testing.assert_array_equal(np.stack([k.numpy() for k in m.track_["mask"]]).astype(np.int8),
                                   gold["track_mask"])
     assert m.best_num_inliers_ == int(gold["best_num_inliers_"])
+    # threshold masks over the supported points (model.py:328,452), as the reference tracked them
+    tm = load_npz("track_thr_ratio08_gm")["threshold_mask"]
+    assert len(m.track_["threshold_mask"]) == tm.shape[0]
+    for k, thm in enumerate(m.track_["threshold_mask"]):
+        sup = tm[k] >= 0
+        np.testing.assert_array_equal(thm.numpy(), tm[k][sup] == 1, err_msg=f"eval {k}")
 
 
 def test_compute_cost_facade_matches_reference():

@@ -227,3 +227,20 @@ def test_oracle_feature_pnp_multi_matches_golden(tag):
     assert initial == pytest.approx(float(z[f"initial_cost_{tag}"]), rel=COST_RTOL)
     assert res["best_cost"] == pytest.approx(float(z[f"best_cost_{tag}"]), rel=COST_RTOL)
     assert res["best_num_inliers"] == int(z[f"best_num_inliers_{tag}"])
+
+
+@pytest.mark.parametrize("name", ["ratio08_gm", "ratio05_sq"])
+def test_oracle_ratio_masks_match_reference_track(name):
+    """track_["threshold_mask"] of the reference's ratio-test runs: the oracle's find_inliers
+    at each tracked pose, restricted to the supported points, is the reference's mask."""
+    inp, meta, gold = case(name)
+    f, _, _ = maps64(inp, orc.sobel)
+    tm = load_npz(f"track_thr_{name}")["threshold_mask"]
+    assert tm.shape[0] == len(gold["track_R"])
+    for k in range(tm.shape[0]):
+        mask, _, nsup = orc.find_inliers(inp["pts3d"], inp["fref"], f, inp["K"], int(inp["im_width"]),
+                                         int(inp["im_height"]), gold["track_R"][k], gold["track_t"][k],
+                                         meta["ratio_threshold"], meta["loss"])
+        sup = tm[k] >= 0
+        assert nsup == int(sup.sum())
+        np.testing.assert_array_equal(mask[sup], tm[k][sup] == 1)
