@@ -109,6 +109,13 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
         // so every CU gets a workgroup; bilinear B=128: G=2 7.32 ms vs G=1 7.75 ms)
         const bool streaming = opt->no_memo || opt->sampling == FMPNP_BILINEAR;
         G = (n <= 0 || (2L * n >= ncu && !streaming)) ? 1 : (ncu + n - 1) / n;
+        // memoised packed-gradient loop on problems of <= 512 points: the evaluation is a
+        // latency chain and a member's exchange costs about what the split saves, so one
+        // workgroup per problem however small the batch (cfg2, ms per launch, G=1 vs the
+        // spread-out G=8: B=8 0.307 vs 0.326, B=16 0.311 vs 0.328, B=32 0.315 vs 0.332,
+        // B=1 0.305 vs 0.313).  Larger problems keep spreading (cfg5, 2048 points at
+        // C=512: G=4 0.64 ms vs G=32 0.58 ms at B=1)
+        if (!streaming && opt->layout == FMPNP_LAYOUT_FGRAD && P.nc_max <= 8) G = 1;
         G = std::max(1, std::min(G, P.nc_max));
     }
     G = std::min(G, MAX_G);

@@ -90,8 +90,9 @@ def test_unaligned_channel_slice_follows_oracle(c_begin, c_end):
 
 
 def test_mixed_sizes_in_one_batch_match_single_launches():
-    """Problems of different N (1..3 blocks) and map sizes in one launch, small enough that
-    the planner forms teams (G > 1): every result equals its single-problem launch."""
+    """Problems of different N (1..3 blocks) and map sizes in one launch with teams of G = 2
+    workgroups (requested: the planner keeps 512-point problems on one workgroup): every
+    result equals its single-problem launch (planner's G = 1)."""
     probs = []
     for s, (n, c, h, w) in enumerate([(37, 8, 30, 40), (130, 16, 60, 80), (64, 12, 45, 50), (190, 4, 20, 30)]):
         inp = synth.problem_inputs(n, c, h, w, seed=40 + s, device=DEV)
@@ -99,8 +100,8 @@ def test_mixed_sizes_in_one_batch_match_single_launches():
         probs.append(rf.make_problem(feats, inp["fref"], inp["pts3d"], inp["K"], inp["im_width"], inp["im_height"],
                                      inp["R0"], inp["t0"]))
     opts = rf.make_options(20, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F64)
-    batch, _ = rf.refine(probs, opts)
-    assert _lib.last_launch()["wgs_per_problem"] > 1
+    batch, _ = rf.refine(probs, rf.make_options(20, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F64, wgs_per_problem=2))
+    assert _lib.last_launch()["wgs_per_problem"] == 2
     for p, rb in zip(probs, batch):
         (r1,), _ = rf.refine([p], opts)
         assert np.array_equal(r1["R"], rb["R"]) and np.array_equal(r1["t"], rb["t"])
