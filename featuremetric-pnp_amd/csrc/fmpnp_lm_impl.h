@@ -375,6 +375,36 @@ __device__ __forceinline__ void gather_half(const T *__restrict__ t, const T *__
     using VT = typename V16<T>::type;
     constexpr int V = V16<T>::n;
     if constexpr (VEC) {
+        if (ce - cb > 64 * V && ce - cb <= 128 * V) {
+            // 64 V < C <= 128 V (C = 512 fp32): all sixteen loads of the four rounds issued
+            // before the first use -- one memory round trip per point instead of two.  Rounds
+            // are consumed in the loop's (r, k) order, so the sums are the loop's bit for bit;
+            // missing rounds read round one again and add exact zeros.
+            const int c = cb + l32 * V;
+            VT f[4], x[4], y[4], q[4];
+            bool has[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                has[r] = c + r * 32 * V < ce;
+                const int cr = has[r] ? c + r * 32 * V : c;
+                f[r] = gload<VT>(t + cr);
+                x[r] = gload<VT>(t + cs + cr);
+                y[r] = gload<VT>(t + 2 * cs + cr);
+                q[r] = gload<VT>(rf + cr);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const T *pf = reinterpret_cast<const T *>(&f[r]), *px = reinterpret_cast<const T *>(&x[r]);
+                const T *py = reinterpret_cast<const T *>(&y[r]), *pr = reinterpret_cast<const T *>(&q[r]);
+#pragma unroll
+                for (int k = 0; k < V; ++k) {
+                    const double z = 0.0;
+                    acc6(a, has[r] ? (double)pf[k] : z, has[r] ? (double)pr[k] : z, has[r] ? (double)px[k] : z,
+                         has[r] ? (double)py[k] : z);
+                }
+            }
+            return;
+        }
         // two rounds per trip, all eight loads issued before the first use (one round trip
         // for C <= 64 V); a missing second round reads round one again and adds exact zeros
         for (int c = cb + l32 * V; c < ce; c += 64 * V) {
