@@ -33,6 +33,21 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 int elem_size(int dtype) { return dtype == FMPNP_F64 ? 8 : 4; }
 
+// Per-problem bounds shared by the LM launch and fmpnp_point_costs: every projected pixel
+// maps to a texel < Hf*Wf through 32-bit unsigned products, and the map size is bounded.
+int validate_problem(const fmpnp_problem &p, int layout) {
+    if (p.N < 0 || p.Hf <= 0 || p.Wf <= 0 || p.im_width <= 0 || p.im_height <= 0) return FMPNP_EINVAL;
+    if (p.c_begin < 0 || p.c_end < p.c_begin || p.c_end > p.cstride || p.c_end > p.ld_ref) return FMPNP_EINVAL;
+    if (p.N > 0 && (!p.feat || !p.fref || !p.pts3d)) return FMPNP_EINVAL;
+    if (layout == FMPNP_LAYOUT_F && (p.Hf >= 65536 || p.Wf >= 65536)) return FMPNP_ETOOBIG;
+    // the packed map must hold 3*cstride per texel
+    if ((long long)p.Hf * p.Wf * 3 * (long long)p.cstride > (1LL << 40)) return FMPNP_ETOOBIG;
+    // pixel -> texel rescale in 32-bit unsigned arithmetic: y * Hf < 2^32, x * Wf < 2^32
+    if ((long long)p.im_height * p.Hf >= (1LL << 32) || (long long)p.im_width * p.Wf >= (1LL << 32))
+        return FMPNP_ETOOBIG;
+    return 0;
+}
+
 int validate(const fmpnp_problem *probs, int n, const fmpnp_options *opt) {
     if (!opt || n < 0 || (n > 0 && !probs)) return FMPNP_EINVAL;
     if (opt->dtype != FMPNP_F32 && opt->dtype != FMPNP_F64) return FMPNP_EINVAL;
@@ -45,16 +60,8 @@ int validate(const fmpnp_problem *probs, int n, const fmpnp_options *opt) {
         return FMPNP_EINVAL;
     if (opt->sobel_flags & ~3) return FMPNP_EINVAL;
     for (int i = 0; i < n; ++i) {
-        const fmpnp_problem &p = probs[i];
-        if (p.N < 0 || p.Hf <= 0 || p.Wf <= 0 || p.im_width <= 0 || p.im_height <= 0) return FMPNP_EINVAL;
-        if (p.c_begin < 0 || p.c_end < p.c_begin || p.c_end > p.cstride || p.c_end > p.ld_ref) return FMPNP_EINVAL;
-        if (p.N > 0 && (!p.feat || !p.fref || !p.pts3d)) return FMPNP_EINVAL;
-        if (opt->layout == FMPNP_LAYOUT_F && (p.Hf >= 65536 || p.Wf >= 65536)) return FMPNP_ETOOBIG;
-        // every projected pixel maps to a texel < Hf*Wf; the packed map must hold 3*cstride per texel
-        if ((long long)p.Hf * p.Wf * 3 * (long long)p.cstride > (1LL << 40)) return FMPNP_ETOOBIG;
-        // pixel -> texel rescale in 32-bit unsigned arithmetic: y * Hf < 2^32, x * Wf < 2^32
-        if ((long long)p.im_height * p.Hf >= (1LL << 32) || (long long)p.im_width * p.Wf >= (1LL << 32))
-            return FMPNP_ETOOBIG;
+        const int rc = validate_problem(probs[i], opt->layout);
+        if (rc) return rc;
     }
     return 0;
 }
@@ -233,10 +240,10 @@ int fmpnp_point_costs(const fmpnp_problem *prob, int layout, int dtype, double *
     if (!prob || !cost || !supported) return FMPNP_EINVAL;
     const fmpnp_problem &p = *prob;
     if (p.N == 0) return 0;
-    if (p.N < 0 || !p.feat || !p.fref || !p.pts3d || p.Hf <= 0 || p.Wf <= 0 || p.im_width <= 0 || p.im_height <= 0)
-        return FMPNP_EINVAL;
-    if (p.c_begin < 0 || p.c_end <= p.c_begin || p.c_end > p.cstride || p.ld_ref < p.c_end) return FMPNP_EINVAL;
     if (layout != FMPNP_LAYOUT_FGRAD && layout != FMPNP_LAYOUT_F) return FMPNP_EINVAL;
+    if (p.c_end <= p.c_begin) return FMPNP_EINVAL;
+    const int rc = validate_problem(p, layout);  // the LM path's bounds (32-bit texel rescale)
+    if (rc) return rc;
     if (dtype != FMPNP_F32 && dtype != FMPNP_F64) return FMPNP_EINVAL;
     if (layout == FMPNP_LAYOUT_F && dtype != FMPNP_F32) return FMPNP_EINVAL;
     return (int)launch_point_costs(p, layout, dtype, cost, supported, (hipStream_t)hip_stream);

@@ -264,14 +264,40 @@ __host__ __device__ __forceinline__ void sincos_small(double x, double &s, doubl
     c = fma(z, pc, 1.0);
 }
 
+// The library sincos for the huge-angle branch below, out of line: its constant tables stay
+// inside the call and never occupy registers of the caller's hot loop.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __attribute__((noinline)) double2 sincos_lib(double x) {
+    double s, c;
+    sincos(x, &s, &c);
+    return make_double2(s, c);
+}
+#else
+inline double2 sincos_lib(double x) {
+    double2 r;
+    r.x = sin(x);
+    r.y = cos(x);
+    return r;
+}
+#endif
+
 // sin, cos of a finite x > pi/4 (a rotation step of more than 45 degrees: rare): Cody-Waite
 // reduction by pi/2 (fdlibm's two-part constant, exact products for |n| < 2^20), then the
 // polynomial above on |r| <= pi/4 and the quadrant swap.  Replaces the library sincos,
 // whose table of 64-bit constants the compiler would otherwise hoist into registers that
-// stay live through the point phase.  Non-finite x gives NaN (as the library does).
+// stay live through the point phase.  Beyond 2^19 pi/2 (|n| >= 2^19: the two-part
+// reduction loses accuracy) the out-of-line library routine (Payne-Hanek) takes over, so
+// every finite step gives the reference's torch.sin / torch.cos (helpers/utils.py:209-221).
+// Non-finite x gives NaN (as the library does).
 __host__ __device__ __forceinline__ void sincos_rr(double x, double &s, double &c) {
     if (!(x < 1e300)) {
         s = c = __builtin_nan("");
+        return;
+    }
+    if (x > 823549.6654402911) {  // 2^19 * pi / 2
+        const double2 r = sincos_lib(x);
+        s = r.x;
+        c = r.y;
         return;
     }
     const double n = rint(x * kc(6.36619772367581382433e-01));  // 2 / pi

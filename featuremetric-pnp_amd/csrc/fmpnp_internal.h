@@ -37,6 +37,9 @@ struct LaunchArgs {
 
 // Fixed LDS head: the LM state + per-problem context (sized generously, 16-B aligned).
 __host__ __device__ constexpr int lds_fixed_bytes() { return 4096; }
+// row stride (doubles) of the LM kernel's structure-of-arrays LDS records: odd, so the
+// writers of one point's fields fall in distinct banks (fmpnp_lm_impl.h lds_X / lds_rec)
+__host__ __device__ constexpr int lds_rs(int mmax) { return mmax + 1; }
 size_t lm_dyn_lds_bytes(int mmax, int nc_max);
 
 hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream);

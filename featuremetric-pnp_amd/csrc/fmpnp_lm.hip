@@ -64,8 +64,9 @@ hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipSt
 }
 
 size_t lm_dyn_lds_bytes(int mmax, int nc_max) {
-    // X[3M] + rec[RECW M] doubles, tex[M] ints (16-B padded), part[nc_max][NV] doubles
-    return (size_t)(3 + RECW) * mmax * 8 + (size_t)((mmax + 3) / 4) * 16 + (size_t)nc_max * NV * 8;
+    // X[3][rs] + rec[RECW][rs] doubles (rs = mmax + 1), tex[M] ints (16-B padded),
+    // part[nc_max][NV] doubles
+    return (size_t)(3 + RECW) * lds_rs(mmax) * 8 + (size_t)((mmax + 3) / 4) * 16 + (size_t)nc_max * NV * 8;
 }
 
 }  // namespace fmpnp

@@ -157,15 +157,19 @@ __device__ __forceinline__ void dbg_stamp(bool on, int k) {
     }
 }
 __device__ __forceinline__ unsigned char *dyn() { return lm_lds + lds_fixed_bytes(); }
-// dynamic carve (mmax = max local points, a multiple of CH):
-//   X[mmax][3], rec[mmax][RECW] doubles, tex[mmax] ints (16-B padded), part[nc_max][NV] doubles
+// dynamic carve (mmax = max local points, a multiple of CH), structure of arrays with the
+// odd row stride rs = lds_rs(mmax) doubles:
+//   X[3][rs], rec[RECW][rs] doubles, tex[mmax] ints (16-B padded), part[nc_max][NV] doubles
+// A lane-per-point read of coordinate / record field k (X[k][i], rec[k][i]) is 64 consecutive
+// doubles: conflict-free.  A gather's six writers (field e6 of one point j) hit banks
+// 2 (e6 rs + j) mod 64, distinct because rs is odd.
 __device__ __forceinline__ double *lds_X(int mmax) { return reinterpret_cast<double *>(dyn()); }
-__device__ __forceinline__ double *lds_rec(int mmax) { return reinterpret_cast<double *>(dyn()) + 3 * mmax; }
+__device__ __forceinline__ double *lds_rec(int mmax) { return reinterpret_cast<double *>(dyn()) + 3 * lds_rs(mmax); }
 __device__ __forceinline__ int *lds_tex(int mmax) {
-    return reinterpret_cast<int *>(reinterpret_cast<double *>(dyn()) + (3 + RECW) * mmax);
+    return reinterpret_cast<int *>(reinterpret_cast<double *>(dyn()) + (3 + RECW) * lds_rs(mmax));
 }
 __device__ __forceinline__ double *lds_part(int mmax) {
-    return reinterpret_cast<double *>(dyn()) + (3 + RECW) * mmax + ((mmax + 3) / 4) * 2;
+    return reinterpret_cast<double *>(dyn()) + (3 + RECW) * lds_rs(mmax) + ((mmax + 3) / 4) * 2;
 }
 
 // so3exp_map (helpers/utils.py:209-221) and the update R' = dR R, t' = dR t + dt
@@ -309,7 +313,8 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
     const Ctx &c = st.c;
     double *X = lds_X(mmax);
     const double *src = c.pts + 3 * (size_t)c.p0;
-    for (int e = tid; e < 3 * c.M; e += NT) X[e] = src[e];
+    const int rs = lds_rs(mmax);
+    for (int e = tid; e < 3 * c.M; e += NT) X[(e % 3) * rs + e / 3] = src[e];
     int *tex = lds_tex(mmax);
     for (int i = tid; i < mmax; i += NT) tex[i] = -2;  // no texel cached yet
     __syncthreads();
@@ -539,14 +544,16 @@ __device__ __forceinline__ constexpr int h_col(int k) {
 // and a harmless geometry (z = 1).  Writes the block's partial (one chunk: LDS when
 // G == 1, the team's global slot `dst_g` with sc1 stores when G > 1).
 __device__ __forceinline__ void contrib_block(const PC &q, int mmax, int blk, bool sup, bool kept, double rho,
-                                              double d1, const double *r, const double Pc[3], double *dst_g) {
+                                              double d1, const double *r, int rs, const double Pc[3],
+                                              double *dst_g) {
     const int lane = threadIdx.x & 63;
     const double fx = q.K[0], fy = q.K[4];
     const int lc = blk;  // one chunk per 64-point block
     const double w = kept ? d1 : 0.0, rh = kept ? rho : 0.0;
     const double P0 = kept ? Pc[0] : 0.0, P1 = kept ? Pc[1] : 0.0, z = kept ? Pc[2] : 1.0;
-    const double sex = kept ? r[1] : 0.0, sey = kept ? r[2] : 0.0;
-    const double sxx = kept ? r[3] : 0.0, sxy = kept ? r[4] : 0.0, syy = kept ? r[5] : 0.0;
+    // the point's record fields (SoA, stride rs): sum gx e, sum gy e, sum gx^2, sum gx gy, sum gy^2
+    const double sex = kept ? r[rs] : 0.0, sey = kept ? r[2 * rs] : 0.0;
+    const double sxx = kept ? r[3 * rs] : 0.0, sxy = kept ? r[4 * rs] : 0.0, syy = kept ? r[5 * rs] : 0.0;
     // J_px_p (model.py:377-382) times J_p_T (model.py:369-370): A (2x6), A0[1] = A1[0] = 0
     // one reciprocal instead of six divisions (Jacobian entries only: last-bit level)
     const double iz = recip(z);
@@ -705,7 +712,7 @@ __device__ __forceinline__ void gather_bil_half(const T *__restrict__ feat, cons
 template <typename T>
 __device__ __forceinline__ void gather_bil_block(unsigned long long m, const Taps &tp, bool hi, int lane,
                                                  const T *feat, const T *fref0, int cs, int cb, int ce, int ld,
-                                                 bool vec, double *rec0, int e6, bool wlane) {
+                                                 bool vec, double *rec0, bool wlane) {
     const int l32 = lane & 31;
     while (m) {
         const int pa = __builtin_ctzll(m);
@@ -730,17 +737,17 @@ __device__ __forceinline__ void gather_bil_block(unsigned long long m, const Tap
         if (vec) gather_bil_half<T, true>(feat, o, w, rf, cs, cb, ce, l32, v);
         else gather_bil_half<T, false>(feat, o, w, rf, cs, cb, ce, l32, v);
         const double r = reduce8_in32(v, lane);
-        if (wlane && (!hi || two)) rec0[(size_t)src * RECW + e6] = r;
+        if (wlane && (!hi || two)) rec0[src] = r;
     }
 }
 
 // Double-buffered pair gathers of one block: the next pair's loads are issued before this
 // pair's channel sums are reduced (one exposed round trip per block, not one per pair).
-// fref0 / rec0: the block's first descriptor row and record.
+// fref0: the block's first descriptor row; rec0: this lane's record field (e6) at the block start.
 template <typename T, bool FULL>
 __device__ __forceinline__ void gather_pipe(unsigned long long m, int off, bool hi, int lane, const T *feat,
                                             const T *fref0, int cs, int ld, int gc1, int gc2, bool has1, bool has2,
-                                            double *rec0, int e6, bool wlane) {
+                                            double *rec0, bool wlane) {
     if (!m) return;
     GLoad<T> A, B;
     GPair pa = pick_pair(m, off, hi), pb;
@@ -755,7 +762,7 @@ __device__ __forceinline__ void gather_pipe(unsigned long long m, int off, bool 
             double v[8];
             g_consume<T, FULL>(A, has1, has2, v);
             const double r = reduce8_in32(v, lane);
-            if (wlane && (!hi || pa.two)) rec0[(size_t)pa.j * RECW + e6] = r;
+            if (wlane && (!hi || pa.two)) rec0[pa.j] = r;
         }
         if (!moreB) break;
         const bool moreA = m != 0;
@@ -767,7 +774,7 @@ __device__ __forceinline__ void gather_pipe(unsigned long long m, int off, bool 
             double v[8];
             g_consume<T, FULL>(B, has1, has2, v);
             const double r = reduce8_in32(v, lane);
-            if (wlane && (!hi || pb.two)) rec0[(size_t)pb.j * RECW + e6] = r;
+            if (wlane && (!hi || pb.two)) rec0[pb.j] = r;
         }
         if (!moreA) break;
     }
@@ -881,7 +888,7 @@ __device__ __forceinline__ void f_issue(FTrip<T> &tr, unsigned long long &m, int
 }
 
 template <typename T, bool FULL>
-__device__ __forceinline__ void f_consume(const FTrip<T> &tr, bool has, bool norm, int lane, double *rec0, int e6,
+__device__ __forceinline__ void f_consume(const FTrip<T> &tr, bool has, bool norm, int lane, double *rec0,
                                           bool wlane) {
     constexpr int V = V16<T>::n;
     double a[8];
@@ -901,7 +908,7 @@ __device__ __forceinline__ void f_consume(const FTrip<T> &tr, bool has, bool nor
     double r = reduce8_in32(a, lane), r2 = r;
     swap32(r, r2);
     r = r + r2;
-    if (wlane && lane < 32) rec0[(size_t)tr.p * RECW + e6] = r;
+    if (wlane && lane < 32) rec0[tr.p] = r;
 }
 
 // Double-buffered form for C <= 64 V with 16-byte loads (one channel round per lane): the
@@ -910,7 +917,7 @@ __device__ __forceinline__ void f_consume(const FTrip<T> &tr, bool has, bool nor
 template <typename T, bool FULL>
 __device__ __forceinline__ void gather_f_pipe(unsigned long long m, int rc, int lane, const T *feat, const T *fref0,
                                               int cs, int cb, int ce, int ld, int Hf, int Wf, bool norm, bool rep,
-                                              double *rec0, int e6, bool wlane) {
+                                              double *rec0, bool wlane) {
     constexpr int V = V16<T>::n;
     if (!m) return;
     const int c0 = cb + lane * V;
@@ -921,11 +928,11 @@ __device__ __forceinline__ void gather_f_pipe(unsigned long long m, int rc, int 
     while (true) {
         const bool moreB = m != 0;
         if (moreB) f_issue<T>(B, m, rc, feat, fref0, cs, ld, c, Hf, Wf, rep);
-        f_consume<T, FULL>(A, has, norm, lane, rec0, e6, wlane);
+        f_consume<T, FULL>(A, has, norm, lane, rec0, wlane);
         if (!moreB) break;
         const bool moreA = m != 0;
         if (moreA) f_issue<T>(A, m, rc, feat, fref0, cs, ld, c, Hf, Wf, rep);
-        f_consume<T, FULL>(B, has, norm, lane, rec0, e6, wlane);
+        f_consume<T, FULL>(B, has, norm, lane, rec0, wlane);
         if (!moreA) break;
     }
 }
@@ -934,7 +941,7 @@ __device__ __forceinline__ void gather_f_pipe(unsigned long long m, int rc, int 
 template <typename T>
 __device__ __forceinline__ void gather_f_block(unsigned long long m, int rc, bool hi, int lane, const T *feat,
                                                const T *fref0, int cs, int cb, int ce, int ld, int Hf, int Wf,
-                                               bool vec, bool norm, bool rep, double *rec0, int e6, bool wlane) {
+                                               bool vec, bool norm, bool rep, double *rec0, bool wlane) {
     while (m) {
         const int p = __builtin_ctzll(m);
         m &= m - 1;
@@ -961,7 +968,7 @@ __device__ __forceinline__ void gather_f_block(unsigned long long m, int rc, boo
         double r = reduce8_in32(v, lane), r2 = r;
         swap32(r, r2);  // the two halves hold the point's even / odd channel groups
         r = r + r2;
-        if (wlane && !hi) rec0[(size_t)p * RECW + e6] = r;
+        if (wlane && !hi) rec0[p] = r;
     }
 }
 
@@ -979,6 +986,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
     const double *X = lds_X(mmax);
     double *rec = lds_rec(mmax);
     int *tex = lds_tex(mmax);
+    const int rs = lds_rs(mmax);
     const T *feat = reinterpret_cast<const T *>(q.feat);
     const T *fref = reinterpret_cast<const T *>(q.fref);
     const int cs = q.cs, cb = q.cb, ce = q.ce, p0 = q.p0, ld = q.ld, M = q.M;
@@ -1012,7 +1020,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         int off = -1, rc = 0;
         Taps tp;
         if (valid) {
-            transform_pt(Re, te, X[3 * i], X[3 * i + 1], X[3 * i + 2], Pc);
+            transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
             int x, y;
             double qx, qy;
             if (project_px(q.K, Pc, q.im_w, q.im_h, x, y, qx, qy)) {
@@ -1034,25 +1042,26 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         dbg_stamp(q.stamps, 0);
         const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
         const bool wlane = (lane & 3) == 0 && e6 < 6;
+        double *recb = rec + (size_t)(wlane ? e6 : 0) * rs + blk * 64;  // this lane's field column
         if constexpr (FL) {
             if (PIPE && vec && ce - cb <= 64 * V)  // one channel round per lane
                 gather_f_pipe<T, true>(m, rc, lane, feat, fref + (size_t)(p0 + blk * 64) * ld, cs, cb, ce, ld, q.Hf,
-                                       q.Wf, q.sob_norm != 0, q.sob_rep != 0, rec + (size_t)blk * 64 * RECW, e6, wlane);
+                                       q.Wf, q.sob_norm != 0, q.sob_rep != 0, recb, wlane);
             else
                 gather_f_block<T>(m, rc, hi, lane, feat, fref + (size_t)(p0 + blk * 64) * ld, cs, cb, ce, ld, q.Hf,
-                                  q.Wf, vec, q.sob_norm != 0, q.sob_rep != 0, rec + (size_t)blk * 64 * RECW, e6, wlane);
+                                  q.Wf, vec, q.sob_norm != 0, q.sob_rep != 0, recb, wlane);
         } else if (q.bilinear) {
             gather_bil_block<T>(m, tp, hi, lane, feat, fref + (size_t)(p0 + blk * 64) * ld, cs, cb, ce, ld, vec,
-                                rec + (size_t)blk * 64 * RECW, e6, wlane);
+                                recb, wlane);
         } else if (PIPE && onetrip) {
             // double-buffered pairs: the next pair's loads are issued before this pair's
             // channel sums are reduced (one exposed round trip per block, not one per pair)
             if (ce - cb == 64 * V)
                 gather_pipe<T, true>(m, off, hi, lane, feat + 0, fref + (size_t)(p0 + blk * 64) * ld, cs, ld, gc1, gc2,
-                                     has1, has2, rec + (size_t)blk * 64 * RECW, e6, wlane);
+                                     has1, has2, recb, wlane);
             else
                 gather_pipe<T, false>(m, off, hi, lane, feat + 0, fref + (size_t)(p0 + blk * 64) * ld, cs, ld, gc1,
-                                      gc2, has1, has2, rec + (size_t)blk * 64 * RECW, e6, wlane);
+                                      gc2, has1, has2, recb, wlane);
         } else {
             while (m) {  // wave-uniform: two dirty points per trip, one per half-wave
                 const GPair pp = pick_pair(m, off, hi);
@@ -1065,7 +1074,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
                 if (vec) gather_half<T, true>(t, rf, cs, cb, ce, l32, v);
                 else gather_half<T, false>(t, rf, cs, cb, ce, l32, v);
                 const double r = reduce8_in32(v, lane);
-                if (wlane && (!hi || pp.two)) rec[(size_t)ii * RECW + e6] = r;
+                if (wlane && (!hi || pp.two)) recb[pp.j] = r;
             }
         }
         // the records just written are read by other lanes of this wave: LDS operations of
@@ -1073,17 +1082,17 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         dbg_stamp(q.stamps, 1);
         const bool sup = off >= 0;
-        const double *r = rec + (size_t)(valid ? i : 0) * RECW;
+        const double *r = rec + (valid ? i : 0);
         double rho = 0.0, d1 = 0.0;
         if (sup) loss_eval(q.loss, q.alpha, 0.5 * r[0], rho, d1);
         if (defer) {
             if (valid) {
-                rec[(size_t)i * RECW + 6] = rho;
-                rec[(size_t)i * RECW + 7] = d1;
+                rec[6 * rs + i] = rho;
+                rec[7 * rs + i] = d1;
             }
             if (sup) lmax = nanmax(lmax, fabs(rho));
         } else {
-            contrib_block(q, mmax, blk, sup, sup, rho, d1, r, Pc, dst_g);
+            contrib_block(q, mmax, blk, sup, sup, rho, d1, r, rs, Pc, dst_g);
         }
         dbg_stamp(q.stamps, 2);
     }
@@ -1098,6 +1107,7 @@ __device__ __forceinline__ void contrib_pass(const PC &q, int mmax) {
     const double *X = lds_X(mmax);
     const double *rec = lds_rec(mmax);
     const int *tex = lds_tex(mmax);
+    const int rs = lds_rs(mmax);
     const double limit = ufirst(st.rho_max) * st.c.ratio_thr;
     double *dst_g = q.part_g;
     if (q.G > 1) dst_g += (size_t)((ufirst((int)st.c.epoch) + 1) & 1) * q.nc_max * NV;
@@ -1111,10 +1121,10 @@ __device__ __forceinline__ void contrib_pass(const PC &q, int mmax) {
         const bool valid = i < q.M;
         const bool sup = valid && tex[i] >= 0;
         double Pc[3] = {0.0, 0.0, 1.0};
-        if (sup) transform_pt(Re, te, X[3 * i], X[3 * i + 1], X[3 * i + 2], Pc);
-        const double *r = rec + (size_t)(valid ? i : 0) * RECW;
-        const bool kept = sup && fabs(r[6]) < limit;
-        contrib_block(q, mmax, blk, sup, kept, r[6], r[7], r, Pc, dst_g);
+        if (sup) transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
+        const double *r = rec + (valid ? i : 0);
+        const bool kept = sup && fabs(r[6 * rs]) < limit;
+        contrib_block(q, mmax, blk, sup, kept, r[6 * rs], r[7 * rs], r, rs, Pc, dst_g);
     }
 }
 

@@ -21,13 +21,13 @@ def configure(**kwargs):
             if k not in _FIND_INLIERS:
                 raise KeyError(f"find_inliers has no parameter {k!r}")
             if isinstance(v, str) and k == "loss_fn":
-                v = losses.BY_NAME[v]
+                v = losses.by_name(v)
             _FIND_INLIERS[k] = v
         elif k in _ADAPTER:
             _ADAPTER[k] = v
         else:
             if isinstance(v, str) and k == "loss_fn":
-                v = losses.BY_NAME[v]
+                v = losses.by_name(v)
             _MODEL[k] = v
 
 

@@ -83,16 +83,27 @@ BY_NAME = {"squared": squared_loss, "huber": huber_loss, "cauchy": cauchy_loss,
            "geman_mcclure": geman_mcclure_loss}
 
 
+def by_name(name):
+    """The loss for a short name ("geman_mcclure") or the reference's function / gin binding
+    name ("geman_mcclure_loss", helpers/utils.py:15-38, default_robotcar.gin:53)."""
+    key = name[:-len("_loss")] if name.endswith("_loss") else name
+    if key not in BY_NAME:
+        raise ValueError(f"unknown loss {name!r}: one of {sorted(BY_NAME)} (optionally with the '_loss' suffix)")
+    return BY_NAME[key]
+
+
 def resolve(loss_fn):
     """(loss code, alpha) of a loss function; only the losses above run on the device."""
     if isinstance(loss_fn, str):
-        loss_fn = BY_NAME[loss_fn]
+        loss_fn = by_name(loss_fn)
     code = getattr(loss_fn, "fmpnp_loss", None)
     if code is None:
+        # the reference's own helpers.utils functions: squared_loss, huber_loss, cauchy_loss,
+        # geman_mcclure_loss (utils.py:15-38)
         name = getattr(loss_fn, "__name__", "")
-        # the reference's own helpers.utils functions carry the same names
-        if name in BY_NAME:
-            return BY_NAME[name].fmpnp_loss, 0.0
-        raise ValueError(f"unsupported loss_fn {loss_fn!r}: use fmpnp.losses.{{squared,huber,cauchy,"
-                         f"geman_mcclure}}_loss or fmpnp.losses.barron(alpha)")
+        try:
+            return by_name(name).fmpnp_loss, 0.0
+        except ValueError:
+            raise ValueError(f"unsupported loss_fn {loss_fn!r}: use fmpnp.losses.{{squared,huber,cauchy,"
+                             f"geman_mcclure}}_loss or fmpnp.losses.barron(alpha)") from None
     return code, getattr(loss_fn, "fmpnp_alpha", 0.0)

@@ -100,6 +100,12 @@ class RefinePipeline:
         pts = [np.asarray(q[2].points_3d, np.float64).reshape(-1, 3) for q in queries]
         n_pts = np.array([a.shape[0] for a in inl], dtype=np.int64)
         fr_off = np.concatenate([[0], np.cumsum(n_pts * css)])
+        # the caller produced the hypercolumns on its own (current) stream: the prep stream
+        # must not read them before that work finished
+        self.prep.wait_stream(torch.cuda.current_stream(dev))
+        for m in qmaps + rmaps:
+            if m.is_cuda:
+                m.record_stream(self.prep)
         with torch.cuda.device(dev), torch.cuda.stream(self.prep):
             def ready(m, dt):  # device, batch dtype, contiguous (else one conversion copy)
                 return m if (m.is_cuda and m.dtype == dt and m.is_contiguous()) else _rf._as_device(m, dev, dt)
@@ -165,7 +171,11 @@ class RefinePipeline:
             if bad:
                 raise IndexError(f"batch {len(out)}: reference inliers of queries {bad} map outside the reference "
                                  "hypercolumn (optimize_feature_pnp.py:56 raises IndexError)")
-            out.append(b.results())
+            res = b.results()
+            # as refine.refine(): a timed-out cross-workgroup exchange left poses unrefined
+            if any(r["status"] & _lib.STATUS_SYNC_TIMEOUT for r in res):
+                raise _lib.FmpnpError(f"batch {len(out)}: cross-workgroup exchange timed out")
+            out.append(res)
 
         for i, queries in enumerate(batches):
             # the host stays at most `depth` batches ahead of the collected results

@@ -224,7 +224,7 @@ def main(argv=None):
     if a.n_iters is not None:
         kw["n_iters"] = a.n_iters
     if a.loss is not None:
-        kw["loss_fn"] = _losses.BY_NAME[a.loss]
+        kw["loss_fn"] = _losses.by_name(a.loss)
     if a.ratio_threshold is not None:
         kw["ratio_threshold"] = a.ratio_threshold
     K = np.load(a.K, allow_pickle=False)

@@ -53,14 +53,29 @@ def reference_descriptors(fmap, X, K, W, H):
     return fmap[:, rows, cols].T.contiguous()
 
 
-def problem_inputs(N=512, C=256, Hf=240, Wf=320, seed=0, device="cuda"):
+def rot_xyz(dx, dy, dz):
+    """Rz(dz) Ry(dy) Rx(dx), degrees (the golden vectors' harder initial rotations)."""
+    ax, ay = math.radians(dx), math.radians(dy)
+    rx = np.array([[1.0, 0.0, 0.0], [0.0, math.cos(ax), -math.sin(ax)], [0.0, math.sin(ax), math.cos(ax)]])
+    ry = np.array([[math.cos(ay), 0.0, math.sin(ay)], [0.0, 1.0, 0.0], [-math.sin(ay), 0.0, math.cos(ay)]])
+    return rot_z(dz) @ ry @ rx
+
+
+# initial poses: "easy" = SURVEY.md §8d (Rz(1 deg), t = (0.05, -0.03, 0.10)); "hard" = the
+# golden vectors' perturbation (tests/golden/gen_golden.py: rot_xyz(0.6, -0.4, 2.0),
+# t = (0.2, -0.12, 0.35)), several texels of image motion per point
+INITS = {"easy": (rot_z(1.0), np.array([0.05, -0.03, 0.10])),
+         "hard": (rot_xyz(0.6, -0.4, 2.0), np.array([0.2, -0.12, 0.35]))}
+
+
+def problem_inputs(N=512, C=256, Hf=240, Wf=320, seed=0, device="cuda", init="easy"):
     """Dict of one query's inputs: fmap [C,Hf,Wf] fp32 (device), fref [N,C] fp32 (device),
     pts3d [N,3] fp64 (numpy), K, im_width, im_height, R0, t0."""
     fmap = feature_map(C, Hf, Wf, seed, device)
     X, K, W, H = scene(N, Hf, Wf, seed)
     fref = reference_descriptors(fmap, X, K, W, H)
-    return dict(fmap=fmap, fref=fref, pts3d=X, K=K, im_width=W, im_height=H, R0=rot_z(1.0),
-                t0=np.array([0.05, -0.03, 0.10]))
+    R0, t0 = INITS[init]
+    return dict(fmap=fmap, fref=fref, pts3d=X, K=K, im_width=W, im_height=H, R0=R0.copy(), t0=t0.copy())
 
 
 # the reference's Prediction fields feature_pnp reads (s2dhm/pose_prediction/solve_pnp.py:7-8)
