@@ -1,27 +1,42 @@
 #!/usr/bin/env python3
-"""Benchmark: feature-metric PnP refinements/s on MI355X (BASELINE.json metric).
+"""Benchmark: feature-metric PnP pose-refinements/s on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1] shape, batched as configs[2]): every GPU refines
-its own batch of B independent queries, each N=512 points, C=256 channels,
-240x320 hypercolumn (960x1280 image, stride 4), Geman-McClure, lambda0=0.01,
-50 LM iterations, fp32 texels / fp64 arithmetic.  Synthetic inputs (SURVEY.md
-§8d recipe; no dataset or CNN weights offline).  One step = one launch of the
-LM kernel over the whole batch (all 50 iterations of all B queries), with the
-packed features already resident in HBM.  Weak scaling: B queries per GPU;
-at 8 GPUs and B=128 this is configs[2] (1024 queries).  No collectives on the
-data path: ranks only meet in the timing barriers.
+Workload (BASELINE.json configs[1] shape, batched as configs[2]): every GPU refines its
+share of independent queries, each N=512 points, C=256 channels, 240x320 hypercolumn
+(960x1280 image, stride 4), Geman-McClure, lambda0=0.01, 50 LM iterations, fp32 texels /
+fp64 arithmetic.  Synthetic inputs (SURVEY.md §8d recipe; no dataset or CNN weights
+offline).  One step = one launch of the LM kernel over the rank's whole batch (all 50
+iterations of all its queries) with the packed features already resident in HBM.
 
-Also reported: single-query latency (B=1, one query spread over several
-workgroups), the feature-pack kernel (fused Sobel + channels-last) rate, the
-end-to-end rate from CHW hypercolumns (pack + reference gather + LM through
-fmpnp.pipeline, wall clock), the roofline of the LM kernel, and the CPU baseline (the oracle's C restatement of
-the reference loop, OpenMP over queries) on a bounded sample.
+Multi-GPU: the queries of a rank are fmpnp.shard.query_indices (the
+global query index also seeds its inputs), timing is fmpnp.shard.timed_steps (barrier +
+synchronise on both sides, max over ranks) -- the same code the gloo tests exercise.
+Default: weak scaling, --batch 128 queries per GPU (configs[2]'s 1024 queries at 8 GPUs);
+--global-batch 1024 is the fixed-total (strong) form.  No collective on the data path.
+
+Roofline (dominant kernel = the LM launch): `achieved` = HBM bytes per launch from the
+committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this exact workload
+(profiles/r02_pmc_<tag>.json, tools/gpu_profile_r02.sh; FETCH_SIZE doubled per
+MI355X_MICROARCH.md) ÷ the launch time measured here with HIP events; without a matching
+profile, the bytes the kernel's gathers move (counted live: texel gathers x 16C + the
+fp64 points).  SURVEY.md §8d's reference-equivalent figure (every point re-read every
+iteration) is reported separately as `reference_equivalent_GBps`: memoised gathers make
+it exceed the HBM peak, so it is not a roofline fraction.
+
+Legs reported beside the headline (rank 0): single query (configs[1]), the fixed total of
+1024 queries on one GPU (SURVEY.md §8e's N=1 point), the harder initialisation and the
+ratio test (input_configs/full_robotcar_08.gin:40), memoisation off, bilinear sampling,
+the f-only layout, the pack kernels, the end-to-end pipeline, and the CPU baselines (C
+restatement of the reference loop, OpenMP over queries; vectorised PyTorch-CPU fp64
+restatement at 1 thread and at every core of the job's share) on a bounded sample whose
+poses are compared with the GPU's for the same queries.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
        N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -34,30 +49,93 @@ import torch  # noqa: E402
 
 N_PTS, C, HF, WF, ITERS = 512, 256, 240, 320, 50
 HBM_PEAK = 8.0e12  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-B_ITER = N_PTS * (16 * C + 24)  # algorithmic bytes per GN iteration per query
+B_ITER = N_PTS * (16 * C + 24)  # SURVEY.md §8d bytes per GN iteration per query (every point re-read)
+LEGS = ["single", "hard", "ratio", "no_memo", "bilinear", "layout_f", "pack", "pipeline", "fixed1024", "cpu"]
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=128, help="queries per GPU")
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=128, help="queries per GPU (weak scaling)")
     ap.add_argument("--global-batch", type=int, default=0,
-                    help="total queries split over the GPUs (strong scaling); 0 = --batch per GPU (weak)")
-    ap.add_argument("--wgs", type=int, default=0, help="workgroups per query (0 = auto)")
-    ap.add_argument("--cpu-sample", type=int, default=1024, help="queries in the CPU-baseline sample (0 = skip)")
+                    help="total queries split over the GPUs (strong scaling); 0 = --batch per GPU")
+    ap.add_argument("--init", choices=["easy", "hard"], default="easy")
+    ap.add_argument("--ratio", type=float, default=None, help="ratio-test threshold (model.py:324-336)")
+    ap.add_argument("--no-memo", action="store_true", help="re-gather every texel at every evaluation")
+    ap.add_argument("--sampling", choices=["nearest", "bilinear"], default="nearest")
+    ap.add_argument("--layout", choices=["fgrad", "f"], default="fgrad")
+    ap.add_argument("--wgs", type=int, default=0, help="workgroups per query (0 = planner)")
+    ap.add_argument("--legs", default="all", help="comma list of " + ",".join(LEGS) + ", or all / none")
+    ap.add_argument("--cpu-sample", type=int, default=1024, help="problems in the C-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--no-extras", action="store_true", help="skip single-query / pack / CPU legs")
-    ap.add_argument("--no-nomemo", action="store_true", help="skip the memoisation-off comparison launch")
-    ap.add_argument("--no-bilinear", action="store_true", help="skip the bilinear-sampling launch")
-    ap.add_argument("--no-pipeline", action="store_true", help="skip the end-to-end (pack + gather + LM) leg")
-    ap.add_argument("--no-layout-f", action="store_true", help="skip the f-only layout launch")
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.legs = set(LEGS) if a.legs == "all" else set() if a.legs == "none" else set(a.legs.split(","))
+    if a.legs - set(LEGS):
+        ap.error(f"unknown legs {sorted(a.legs - set(LEGS))}")
+    return a
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def workload_tag(B, init, ratio, memo, sampling, layout):
+    """Key of a workload in profiles/r02_pmc_<tag>.json."""
+    t = f"b{B}_{init}"
+    if ratio is not None:
+        t += f"_ratio{ratio:g}"
+    if not memo:
+        t += "_nomemo"
+    if sampling != "nearest":
+        t += "_" + sampling
+    if layout != "fgrad":
+        t += "_layout" + layout
+    return t
+
+
+def load_traffic(tag):
+    """(HBM bytes per launch, kernel name, rocprof avg ns) of a workload from its committed
+    rocprofv3 PMC summary, or (None, None, None)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", f"r02_pmc_{tag}.json")) as f:
+            d = json.load(f)
+        name = (d.get("kernel") or "").replace("void ", "").replace("(fmpnp::LaunchArgs)", "")
+        return d.get("hbm_bytes_per_launch"), name or None, d.get("kernel_avg_ns")
+    except (OSError, ValueError):
+        return None, None, None
+
+
+def gather_bytes_rule(sampling, layout):
+    """Bytes one texel gather moves (fp32) and the rule's text."""
+    if layout == "f":
+        return 40 * C, "9 neighbour texels x 4C (f) + 4C fref per gather"
+    if sampling == "bilinear":
+        return 52 * C, "4 taps x (f, gx, gy) 4C + 4C fref per sampled point"
+    return 16 * C, "(f, gx, gy, fref) x 4C per gather"
+
+
+def roofline(tag, res, kernel_s, B, sampling, layout):
+    per_gather, rule = gather_bytes_rule(sampling, layout)
+    gathers = int(sum(r["texel_gathers"] for r in res))
+    n_evals = int(sum(r["n_evals"] for r in res))
+    gathered = gathers * per_gather + B * N_PTS * 24
+    traffic, kname, prof_ns = load_traffic(tag)
+    ach_bytes = traffic if traffic else gathered
+    ach = ach_bytes / kernel_s
+    return {"bound": "hbm", "achieved": round(ach / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK, 4), "traffic": traffic,
+            "achieved_source": ("rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r02_pmc_%s.json" % tag) if traffic
+            else "texel gathers counted by the kernel x bytes per gather (no matching PMC profile)",
+            "kernel": kname or "fmpnp::lm_kernel", "avg_kernel_ms": round(kernel_s * 1e3, 4),
+            "rocprof_avg_kernel_ms": round(prof_ns / 1e6, 4) if prof_ns else None,
+            "gathered_bytes_per_launch": gathered, "gathered_GB_per_s": round(gathered / kernel_s / 1e9, 1),
+            "gathered_bytes_rule": rule + " + 24 B fp64 point per query point",
+            "texel_gathers_per_point_eval": round(gathers / max(1, n_evals * N_PTS), 4),
+            "reference_equivalent_GBps": round(B * ITERS * B_ITER / kernel_s / 1e9, 1),
+            "reference_equivalent_rule": "SURVEY.md 8d: B * iters * N*(16C+24) -- every point's texel re-read at "
+                                         "every iteration, as the reference does; not a roofline fraction"}
 
 
 def main():
@@ -80,30 +158,28 @@ def main():
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
 
-    import fmpnp
-    from fmpnp import _lib, refine as rf, synth
+    from fmpnp import _lib, refine as rf, shard, synth
 
     # ---------------- setup (untimed): this rank's queries, packed in HBM ----------------
-    # weak scaling (default): B queries per GPU; --global-batch G: G queries split over the
-    # ranks (SURVEY.md 8e's fixed-total form, e.g. 1024), strong scaling
-    B = -(-args.global_batch // world) if args.global_batch > 0 else args.batch
+    qidx = shard.query_indices(rank, world, per_rank=args.batch, global_batch=args.global_batch)
+    B = len(qidx)
+    memo = not args.no_memo
     t0 = time.time()
-    probs = []
-    keep = []
-    for q in range(B):
-        seed = rank * 100003 + q
-        inp = synth.problem_inputs(N_PTS, C, HF, WF, seed=seed, device=dev)
-        feats = rf.pack_features(inp["fmap"], storage=torch.float32, device=dev)
-        probs.append(rf.make_problem(feats, inp["fref"], inp["pts3d"], inp["K"], inp["im_width"],
-                                     inp["im_height"], inp["R0"], inp["t0"]))
-        if q < 1:
-            keep.append(inp)
-        del inp
+    feats, inputs, probs = [], [], []
+    for q in qidx:
+        inp = synth.problem_inputs(N_PTS, C, HF, WF, seed=q, device=dev, init=args.init)
+        f = rf.pack_features(inp["fmap"], storage=torch.float32, device=dev, layout=args.layout)
+        probs.append(rf.make_problem(f, inp["fref"], inp["pts3d"], inp["K"], inp["im_width"], inp["im_height"],
+                                     inp["R0"], inp["t0"]))
+        feats.append(f)
+        inp.pop("fmap")
+        inputs.append(inp)
     torch.cuda.synchronize()
     if rank == 0:
         log(f"[bench] setup {B} queries/GPU in {time.time() - t0:.1f}s "
             f"({torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB resident)")
-    opts = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32, wgs_per_problem=args.wgs)
+    opts = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, ratio_threshold=args.ratio, dtype=_lib.F32,
+                           wgs_per_problem=args.wgs, memoize=memo, sampling=args.sampling)
     batch = rf.AsyncBatch(probs, opts)
 
     # ---------------- warmup ----------------
@@ -112,134 +188,29 @@ def main():
     torch.cuda.synchronize()
     launch = _lib.last_launch()
 
-    # ---------------- timed region ----------------
-    stream = torch.cuda.current_stream(dev)
+    # ---------------- timed region: exactly K launches ----------------
+    stream = torch.cuda.current_stream(dev)  # the stream the launches go to (_lib.stream_ptr)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for k in range(args.steps):
+
+    def step(k):
         ev[k][0].record(stream)
         batch.launch()
         ev[k][1].record(stream)
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    elapsed = time.perf_counter() - t_start
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    if dist:
-        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
+
+    elapsed = shard.timed_steps(step, args.steps, device=dev)
+    kernel_s = float(np.mean([a.elapsed_time(b) for a, b in ev])) / 1e3
     res = batch.results()
     statuses = sorted({r["status"] for r in res})
     if any(s & _lib.STATUS_SYNC_TIMEOUT for s in statuses):
         raise RuntimeError("sync timeout in the LM kernel")
-
     value = B * world * args.steps / elapsed
-    ms_step = 1e3 * elapsed / args.steps
-    avg_kernel_s = float(np.mean(kern_ms)) / 1e3
-    algo_bytes = B * ITERS * B_ITER
-    achieved = algo_bytes / avg_kernel_s
-    # bytes the memoised kernel actually gathers: 16C per point-texel gather (f, gx, gy, fref
-    # fp32) + the fp64 points read once per query
-    gathers = int(sum(r["texel_gathers"] for r in res))
-    gathered_bytes = gathers * 16 * C + B * N_PTS * 24
-    n_evals = int(sum(r["n_evals"] for r in res))
-
-    # the same launch with memoisation off: every point's texel re-read at every evaluation,
-    # i.e. the reference's data movement -- the HBM-bound form of the loop
-    nm = {}
-    if not args.no_nomemo:
-        opts_nm = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32, wgs_per_problem=args.wgs,
-                                  memoize=False)
-        batch_nm = rf.AsyncBatch(probs, opts_nm)
-        batch_nm.launch()
-        torch.cuda.synchronize()
-        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = max(1, min(args.steps, 5))
-        s_ev.record(stream)
-        for _ in range(reps):
-            batch_nm.launch()
-        e_ev.record(stream)
-        torch.cuda.synchronize()
-        nm_s = s_ev.elapsed_time(e_ev) / reps / 1e3
-        res_nm = batch_nm.results()
-        same = all(np.array_equal(a["R"], b["R"]) and np.array_equal(a["t"], b["t"]) for a, b in zip(res, res_nm))
-        nm_bytes = int(sum(r["texel_gathers"] for r in res_nm)) * 16 * C + B * N_PTS * 24
-        nm = {"ms_per_launch": round(nm_s * 1e3, 4), "pose_refinements_per_s": round(B / nm_s, 1),
-              "gathered_bytes_per_launch": nm_bytes, "achieved_GB_per_s": round(nm_bytes / nm_s / 1e9, 1),
-              "frac": round(nm_bytes / nm_s / HBM_PEAK, 4), "poses_bit_identical_to_memoised": bool(same)}
-        del batch_nm
-
-    # FMPNP_LAYOUT_F: the same queries with only the f plane in HBM (the LM gather forms the
-    # Sobel gradients), plus that layout's pack kernel (a channels-last copy)
-    lf = {}
-    if not args.no_layout_f:
-        keep_f = []
-        for q in range(B):
-            inp = synth.problem_inputs(N_PTS, C, HF, WF, seed=rank * 100003 + q, device=dev)
-            feats = rf.pack_features(inp["fmap"], storage=torch.float32, device=dev, layout="f")
-            keep_f.append(rf.make_problem(feats, inp["fref"], inp["pts3d"], inp["K"], inp["im_width"],
-                                          inp["im_height"], inp["R0"], inp["t0"]))
-            del inp
-        batch_f = rf.AsyncBatch(keep_f, opts)
-        batch_f.launch()
-        torch.cuda.synchronize()
-        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = max(1, min(args.steps, 5))
-        s_ev.record(stream)
-        for _ in range(reps):
-            batch_f.launch()
-        e_ev.record(stream)
-        torch.cuda.synchronize()
-        f_s = s_ev.elapsed_time(e_ev) / reps / 1e3
-        res_f = batch_f.results()
-        f_gath = int(sum(r["texel_gathers"] for r in res_f))
-        lf = {"ms_per_launch": round(f_s * 1e3, 4), "pose_refinements_per_s": round(B / f_s, 1),
-              "gathered_bytes_per_launch": f_gath * 40 * C + B * N_PTS * 24,
-              "bytes_rule": "per texel gather 9 neighbours x 4C (f) + 4C fref; fp64 point",
-              "max_rot_diff_vs_fgrad_rad": float(max(np.arccos(np.clip((np.trace(a["R"].T @ b["R"]) - 1) / 2, -1, 1))
-                                                     for a, b in zip(res, res_f))),
-              "statuses": sorted({r["status"] for r in res_f})}
-        del batch_f, keep_f
-
-    # bilinear sampling (extension, FMPNP_BILINEAR): every supported point reads its 2x2 taps
-    # of f, gx, gy plus fref at every evaluation -- SURVEY.md 8d's N*(52C+24) bytes per GN
-    # iteration, no memoisation: the bandwidth-bound form of the loop
-    bil = {}
-    if not args.no_bilinear:
-        opts_b = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32, wgs_per_problem=args.wgs,
-                                 sampling="bilinear")
-        batch_b = rf.AsyncBatch(probs, opts_b)
-        batch_b.launch()
-        torch.cuda.synchronize()
-        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = max(1, min(args.steps, 3))
-        s_ev.record(stream)
-        for _ in range(reps):
-            batch_b.launch()
-        e_ev.record(stream)
-        torch.cuda.synchronize()
-        b_s = s_ev.elapsed_time(e_ev) / reps / 1e3
-        res_b = batch_b.results()
-        b_evals = int(sum(r["n_evals"] for r in res_b))
-        b_bytes = b_evals * N_PTS * (52 * C + 24)  # every evaluation samples every point (upper bound)
-        bil = {"ms_per_launch": round(b_s * 1e3, 4), "pose_refinements_per_s": round(B / b_s, 1),
-               "gn_iters_per_s": round(B * ITERS / b_s, 1), "algorithmic_bytes_per_launch": b_bytes,
-               "bytes_rule": "SURVEY.md 8d bilinear: N*(52C+24) per point-evaluation (4 taps x f,gx,gy + fref "
-                             "fp32, fp64 point)",
-               "achieved_GB_per_s": round(b_bytes / b_s / 1e9, 1), "frac": round(b_bytes / b_s / HBM_PEAK, 4),
-               "statuses": sorted({r["status"] for r in res_b})}
-        del batch_b
+    tag = workload_tag(B, args.init, args.ratio, memo, args.sampling, args.layout)
 
     extras = {}
-    if rank == 0 and not args.no_extras:
-        extras = run_extras(args, dev, probs, keep, opts, rf, _lib, synth)
+    if rank == 0 and args.legs:
+        extras = run_legs(args, dev, probs, feats, inputs, opts, res, rf, _lib, synth)
 
     if rank == 0:
-        traffic, traffic_kernel = load_traffic(B)
         out = {
             "metric": "pose-refinements/sec (N=512 pts, C=256, 240x320, 50 LM iters)",
             "value": round(value, 3),
@@ -247,38 +218,24 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_step, 4),
+            "ms_per_step": round(1e3 * elapsed / args.steps, 4),
             "higher_is_better": True,
             "scaling": "strong" if args.global_batch > 0 else "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (SURVEY.md §8d: smoothed L2-normalised random hypercolumns, seeded points)",
-            "config": {"workload": "configs[1] shape batched as configs[2]: B independent queries per GPU "
-                                   "(B=128 x 8 GPUs = 1024)",
+            "data": "synthetic (SURVEY.md §8d: smoothed L2-normalised random hypercolumns, seeded points; "
+                    "seed = global query index)",
+            "config": {"workload": "configs[1] shape batched as configs[2]: "
+                                   + (f"{args.global_batch} queries split over the GPUs" if args.global_batch
+                                      else f"{args.batch} independent queries per GPU (x8 GPUs = 1024)"),
                        "points": N_PTS, "channels": C, "feature_map": f"{HF}x{WF}", "image": f"{4 * HF}x{4 * WF}",
                        "iters": ITERS, "loss": "geman_mcclure", "lambda0": 0.01, "texel_storage": "f32",
+                       "init": args.init, "ratio_threshold": args.ratio, "memoised": memo,
+                       "sampling": args.sampling, "layout": args.layout,
                        "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": f"query sharding x{world} (no collectives)",
-                       "launch": launch},
+                       "parallelism": f"query sharding x{world} (no collectives)", "launch": launch},
             "gn_iters_per_s": round(value * ITERS, 1),
-            "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
-                         "traffic": traffic,
-                         "kernel": traffic_kernel or "fmpnp::lm_kernel<float, 2, false, false, true>",
-                         "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
-                         "algorithmic_bytes_per_launch": algo_bytes,
-                         "bytes_rule": "SURVEY.md 8d: B * iters * N*(16C+24) (f, gx, gy, fref fp32 at one "
-                                       "texel + fp64 point per GN iteration)",
-                         "gathered_bytes_per_launch": gathered_bytes,
-                         "gathered_GB_per_s": round(gathered_bytes / avg_kernel_s / 1e9, 1),
-                         "texel_gathers_per_point_eval": round(gathers / max(1, n_evals * N_PTS), 4),
-                         "note": "achieved counts the reference's data movement; the kernel re-reads a "
-                                 "texel only when a point's pixel changed (bit-identical), so achieved > "
-                                 "peak is possible; gathered_* is what it actually reads, no_memo the "
-                                 "HBM-bound form"},
-            "no_memo": nm,
-            "bilinear": bil,
-            "layout_f": lf,
+            "roofline": roofline(tag, res, kernel_s, B, args.sampling, args.layout),
             "statuses": statuses,
         }
         out.update(extras)
@@ -288,153 +245,280 @@ def main():
         tdist.destroy_process_group()
 
 
-def load_traffic(B):
-    """(HBM bytes per launch, kernel name) from the committed rocprofv3 PMC summary of this
-    workload (profiles/pmc_traffic.json, tools/gpu_profile.sh), if any."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        if d.get("batch") == B:
-            name = (d.get("kernel") or "").replace("void ", "").replace("(fmpnp::LaunchArgs)", "")
-            return d.get("hbm_bytes_per_launch"), name or None
-    except (OSError, ValueError):
-        pass
-    return None, None
-
-
-def run_extras(args, dev, probs, keep, opts, rf, _lib, synth):
-    out = {}
-    # single-query latency: one query, workgroups of a team cooperate on its points
-    one = rf.AsyncBatch(probs[:1], opts)
-    for _ in range(3):
-        one.launch()
+def time_launches(batch, reps, stream):
+    """Mean ms per launch over `reps` back-to-back launches (after one warm-up), results."""
+    batch.launch()
     torch.cuda.synchronize()
-    reps = 20
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
+    s.record(stream)
     for _ in range(reps):
-        one.launch()
-    e.record()
+        batch.launch()
+    e.record(stream)
     torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / reps
-    out["single_query"] = {"ms_per_refinement": round(ms, 4), "gn_iters_per_s": round(ITERS / (ms / 1e3), 1),
-                           "launch": _lib.last_launch()}
-    # feature pack kernel (fused Sobel + channels-last): 4C bytes read + 12C written per texel.
-    # Rotates over NP distinct maps and output buffers (NP x 314.6 MB > the 256 MB Infinity
-    # Cache) so every launch streams from / to HBM.
-    import ctypes
-    L = _lib.load()
-    st = _lib.stream_ptr(dev)
-    NP = 4
-    fms = [synth.feature_map(C, HF, WF, 777 + i, dev) for i in range(NP)]
-    outs = [torch.empty((HF, WF, 3, C), dtype=torch.float32, device=dev) for _ in range(NP)]
+    return s.elapsed_time(e) / reps, batch.results()
 
-    def pack(i):
-        rc = L.fmpnp_pack_features(ctypes.c_void_p(fms[i % NP].data_ptr()), None, None, _lib.F32, C, HF, WF,
-                                   ctypes.c_void_p(outs[i % NP].data_ptr()), _lib.F32, C, 0, 0, st)
-        _lib.check(rc, "pack")
-    for i in range(NP):
-        pack(i)
-    torch.cuda.synchronize()
-    reps = 8 * NP
-    s.record(torch.cuda.current_stream(dev))
-    for i in range(reps):
-        pack(i)
-    e.record(torch.cuda.current_stream(dev))
-    torch.cuda.synchronize()
-    pms = s.elapsed_time(e) / reps
-    pbytes = 16 * C * HF * WF
-    out["pack"] = {"ms": round(pms, 4), "GB_per_s": round(pbytes / (pms / 1e3) / 1e9, 1),
-                   "frac_of_peak": round(pbytes / (pms / 1e3) / HBM_PEAK, 4),
-                   "bytes_rule": "16C per texel (4C read + 12C written), %d distinct maps rotated" % NP}
-    # the f-only layout's pack (FMPNP_LAYOUT_F): a channels-last copy, 4C read + 4C written
-    outs_f = [torch.empty((HF, WF, C), dtype=torch.float32, device=dev) for _ in range(NP)]
 
-    def pack_f(i):
-        rc = L.fmpnp_pack_features_f(ctypes.c_void_p(fms[i % NP].data_ptr()), _lib.F32, C, HF, WF,
-                                     ctypes.c_void_p(outs_f[i % NP].data_ptr()), _lib.F32, C, st)
-        _lib.check(rc, "pack_f")
-    for i in range(NP):
-        pack_f(i)
-    torch.cuda.synchronize()
-    s.record(torch.cuda.current_stream(dev))
-    for i in range(reps):
-        pack_f(i)
-    e.record(torch.cuda.current_stream(dev))
-    torch.cuda.synchronize()
-    fms_ = s.elapsed_time(e) / reps
-    fbytes = 8 * C * HF * WF
-    out["pack_f"] = {"ms": round(fms_, 4), "GB_per_s": round(fbytes / (fms_ / 1e3) / 1e9, 1),
-                     "frac_of_peak": round(fbytes / (fms_ / 1e3) / HBM_PEAK, 4),
-                     "bytes_rule": "8C per texel (4C read + 4C written), %d distinct maps rotated" % NP}
-    del outs_f
-    del fms, outs
-    # end to end from CHW hypercolumns (fmpnp.pipeline.RefinePipeline): pack + reference
-    # gather + LM per batch, preparation of batch i+1 on a second stream under batch i's LM
-    if not args.no_pipeline:
-        import fmpnp
-        from fmpnp.pipeline import RefinePipeline
-        nb, qb = 4, 64
-        batches, img = synth.pipeline_queries(nb, qb, N_PTS, C, HF, WF, device=dev, seed0=5000)
-        pipe = RefinePipeline(img, storage=torch.float32, depth=2,
-                              model_kwargs=dict(n_iters=ITERS, loss_fn=fmpnp.geman_mcclure_loss, lambda_=0.01,
-                                                ratio_threshold=None))
-        pipe.run(batches)  # sizes the slab ring
-        best = None
-        for _ in range(3):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            res = pipe.run(batches)
-            torch.cuda.synchronize()
-            dt = time.perf_counter() - t0
-            best = dt if best is None else min(best, dt)
-        out["end_to_end"] = {"queries_per_s": round(nb * qb / best, 1), "ms_per_query": round(best / (nb * qb) * 1e3, 4),
-                             "batches": nb, "batch": qb,
-                             "statuses": sorted({r["status"] for b in res for r in b}),
-                             "note": "wall clock, host included: Sobel+pack and reference gather of every "
-                                     "query (distinct maps) + one LM launch per batch, two streams"}
-        del batches, pipe
-    # CPU baseline: the oracle (C restatement of the reference loop), OpenMP over queries
-    if args.cpu_sample > 0 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
-        out["cpu_baseline"] = cpu_baseline(args, keep[0])
+def rot_angle(Ra, Rb):
+    c = (np.trace(np.asarray(Ra).T @ np.asarray(Rb)) - 1.0) / 2.0
+    return math.acos(max(-1.0, min(1.0, c)))
+
+
+def leg_summary(tag, ms, res, B, sampling="nearest", layout="fgrad", base=None):
+    rf_s = B / (ms / 1e3)
+    d = {"ms_per_launch": round(ms, 4), "pose_refinements_per_s": round(rf_s, 1),
+         "gn_iters_per_s": round(rf_s * ITERS, 1), "statuses": sorted({r["status"] for r in res}),
+         "roofline": roofline(tag, res, ms / 1e3, B, sampling, layout)}
+    if base is not None:
+        d["max_rot_diff_vs_headline_rad"] = float(max(rot_angle(a["R"], b["R"]) for a, b in zip(res, base)))
+        d["poses_bit_identical_to_headline"] = bool(all(np.array_equal(a["R"], b["R"]) and
+                                                        np.array_equal(a["t"], b["t"]) for a, b in zip(res, base)))
+    return d
+
+
+def run_legs(args, dev, probs, feats, inputs, opts, res_main, rf, _lib, synth):
+    out = {}
+    stream = torch.cuda.current_stream(dev)
+    B = len(probs)
+    memo = not args.no_memo
+
+    def opt(**kw):
+        base = dict(ratio_threshold=args.ratio, dtype=_lib.F32, wgs_per_problem=args.wgs, memoize=memo,
+                    sampling=args.sampling)
+        base.update(kw)
+        return rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, **base)
+
+    if "single" in args.legs:  # configs[1]: one query, one launch
+        ms, r1 = time_launches(rf.AsyncBatch(probs[:1], opts), 20, stream)
+        out["single_query"] = {"ms_per_refinement": round(ms, 4), "gn_iters_per_s": round(ITERS / (ms / 1e3), 1),
+                               "launch": _lib.last_launch()}
+    # the harder initialisation (golden vectors' perturbation): same maps, other start poses
+    if "hard" in args.legs and args.init == "easy":
+        R0, t0 = synth.INITS["hard"]
+        hp = [rf.make_problem(p.feats, p.fref, p.pts3d, p.K, p.im_width, p.im_height, R0, t0) for p in probs]
+        ms, r = time_launches(rf.AsyncBatch(hp, opts), 10, stream)
+        out["hard_init"] = leg_summary(workload_tag(B, "hard", args.ratio, memo, args.sampling, args.layout),
+                                       ms, r, B, args.sampling, args.layout)
+        if "ratio" in args.legs:
+            ms, r = time_launches(rf.AsyncBatch(hp, opt(ratio_threshold=0.8)), 10, stream)
+            out["hard_init_ratio08"] = leg_summary(workload_tag(B, "hard", 0.8, memo, args.sampling, args.layout),
+                                                   ms, r, B, args.sampling, args.layout)
+            out["hard_init_ratio08"]["kernel_variant"] = "RATIO=true"
+        del hp
+    if "ratio" in args.legs and args.ratio is None:  # input_configs/full_robotcar_08.gin:40
+        ms, r = time_launches(rf.AsyncBatch(probs, opt(ratio_threshold=0.8)), 10, stream)
+        out["ratio08"] = leg_summary(workload_tag(B, args.init, 0.8, memo, args.sampling, args.layout), ms, r, B,
+                                     args.sampling, args.layout)
+        out["ratio08"]["kernel_variant"] = "RATIO=true"
+    if "no_memo" in args.legs and memo:  # the reference's data movement: every texel re-read
+        ms, r = time_launches(rf.AsyncBatch(probs, opt(memoize=False)), 5, stream)
+        out["no_memo"] = leg_summary(workload_tag(B, args.init, args.ratio, False, args.sampling, args.layout), ms,
+                                     r, B, args.sampling, args.layout, base=res_main)
+    if "bilinear" in args.legs and args.sampling == "nearest" and args.layout == "fgrad":  # extension
+        ms, r = time_launches(rf.AsyncBatch(probs, opt(sampling="bilinear")), 3, stream)
+        out["bilinear"] = leg_summary(workload_tag(B, args.init, args.ratio, memo, "bilinear", "fgrad"), ms, r, B,
+                                      "bilinear", "fgrad")
+    if "layout_f" in args.legs and args.layout == "fgrad" and args.sampling == "nearest":
+        fp = []
+        for q, inp in enumerate(inputs):
+            fm = synth.feature_map(C, HF, WF, q, dev)  # rank 0: query q has global index (seed) q
+            ff = rf.pack_features(fm, storage=torch.float32, device=dev, layout="f")
+            fp.append(rf.make_problem(ff, probs[q].fref, probs[q].pts3d, inp["K"], inp["im_width"],
+                                      inp["im_height"], inp["R0"], inp["t0"]))
+            del fm
+        ms, r = time_launches(rf.AsyncBatch(fp, opts), 5, stream)
+        out["layout_f"] = leg_summary(workload_tag(B, args.init, args.ratio, memo, "nearest", "f"), ms, r, B,
+                                      "nearest", "f", base=res_main)
+        del fp
+    if "pack" in args.legs:
+        out.update(pack_legs(dev, _lib, synth))
+    if "pipeline" in args.legs:
+        out["end_to_end"] = pipeline_leg(dev, synth)
+    if "fixed1024" in args.legs and B < 1024 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        out["fixed_total_1024"] = fixed_total_leg(args, dev, probs, feats, inputs, opts, rf, synth, stream)
+    if "cpu" in args.legs and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        out["cpu_baseline"] = cpu_baseline(args, res_main, synth, dev)
     return out
 
 
-def cpu_baseline(args, inp0):
-    import oracle.oracle as orc
-    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    n_maps = min(threads, args.cpu_sample)
-    from fmpnp import synth
-    maps = []
-    for m in range(n_maps):
-        inp = synth.problem_inputs(N_PTS, C, HF, WF, seed=900000 + m, device="cpu")
-        fm = inp["fmap"].double().numpy()
-        gx, gy = orc.sobel(fm)
-        maps.append((inp, fm, gx, gy))
-    probs = []
-    for q in range(args.cpu_sample):
-        inp, fm, gx, gy = maps[q % n_maps]
-        probs.append(orc.make_problem(inp["pts3d"], inp["fref"].double().numpy(), fm, gx, gy, inp["K"],
-                                      inp["im_width"], inp["im_height"], inp["R0"], inp["t0"]))
-    opts = orc.make_options(ITERS, 0.01, "geman_mcclure")
-    orc.lib()
-    t = time.perf_counter()
-    orc.forward_batch(probs, opts, threads)
-    dt = time.perf_counter() - t
-    cpu_model = ""
+def fixed_total_leg(args, dev, probs, feats, inputs, opts, rf, synth, stream):
+    """SURVEY.md §8e's fixed total of 1024 queries on ONE GPU (the N=1 point of the strong-scaling
+    curve): the headline's queries plus the next ones by global index, one launch.  Packed
+    layout when it fits in HBM (1024 x 236 MB), else the f-only layout."""
+    from fmpnp import _lib
+    n = 1024
+    torch.cuda.synchronize()
+    free, _ = torch.cuda.mem_get_info(dev)
+    need = (n - len(probs)) * (HF * WF * 3 * C * 4 + N_PTS * C * 4 + N_PTS * 24) + (8 << 30)
+    layout = args.layout if free > need else "f"
+    if layout != args.layout:
+        probs, feats = [], []
+    ps = list(probs)
+    for q in range(len(ps), n):
+        inp = synth.problem_inputs(N_PTS, C, HF, WF, seed=q, device=dev, init=args.init)
+        f = rf.pack_features(inp["fmap"], storage=torch.float32, device=dev, layout=layout)
+        ps.append(rf.make_problem(f, inp["fref"], inp["pts3d"], inp["K"], inp["im_width"], inp["im_height"],
+                                  inp["R0"], inp["t0"]))
+        del inp
+    ms, r = time_launches(rf.AsyncBatch(ps, opts), 5, stream)
+    d = leg_summary(workload_tag(n, args.init, args.ratio, not args.no_memo, args.sampling, layout), ms, r, n,
+                    args.sampling, layout)
+    d.update(layout=layout, launch=_lib.last_launch(),
+             resident_GiB=round(torch.cuda.memory_allocated(dev) / 2**30, 1))
+    del ps
+    torch.cuda.empty_cache()
+    return d
+
+
+def pack_legs(dev, _lib, synth):
+    """The feature-pack kernels (fused Sobel + channels-last; f-only copy), rotating over NP
+    distinct maps and outputs (NP x 314.6 MB > the 256 MB Infinity Cache: HBM-streamed)."""
+    import ctypes
+    out = {}
+    L = _lib.load()
+    st = _lib.stream_ptr(dev)
+    stream = torch.cuda.current_stream(dev)
+    NP = 4
+    fms = [synth.feature_map(C, HF, WF, 777 + i, dev) for i in range(NP)]
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for name, planes, fn in (("pack", 3, L.fmpnp_pack_features), ("pack_f", 1, L.fmpnp_pack_features_f)):
+        outs = [torch.empty((HF, WF, planes, C), dtype=torch.float32, device=dev) for _ in range(NP)]
+
+        def run(i):
+            if planes == 3:
+                rc = fn(ctypes.c_void_p(fms[i % NP].data_ptr()), None, None, _lib.F32, C, HF, WF,
+                        ctypes.c_void_p(outs[i % NP].data_ptr()), _lib.F32, C, 0, 0, st)
+            else:
+                rc = fn(ctypes.c_void_p(fms[i % NP].data_ptr()), _lib.F32, C, HF, WF,
+                        ctypes.c_void_p(outs[i % NP].data_ptr()), _lib.F32, C, st)
+            _lib.check(rc, name)
+        for i in range(NP):
+            run(i)
+        torch.cuda.synchronize()
+        reps = 8 * NP
+        s.record(stream)
+        for i in range(reps):
+            run(i)
+        e.record(stream)
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / reps
+        nbytes = (4 + 4 * planes) * C * HF * WF
+        out[name] = {"ms": round(ms, 4), "GB_per_s": round(nbytes / (ms / 1e3) / 1e9, 1),
+                     "frac_of_peak": round(nbytes / (ms / 1e3) / HBM_PEAK, 4),
+                     "bytes_rule": f"{4 + 4 * planes}C per texel (4C read + {4 * planes}C written), "
+                                   f"{NP} distinct maps rotated"}
+        del outs
+    del fms
+    return out
+
+
+def pipeline_leg(dev, synth):
+    """End to end from CHW hypercolumns (fmpnp.pipeline.RefinePipeline): pack + reference
+    gather + LM per batch, preparation of batch i+1 on a second stream under batch i's LM."""
+    import fmpnp
+    from fmpnp.pipeline import RefinePipeline
+    nb, qb = 4, 64
+    batches, img = synth.pipeline_queries(nb, qb, N_PTS, C, HF, WF, device=dev, seed0=5000)
+    pipe = RefinePipeline(img, storage=torch.float32, depth=2,
+                          model_kwargs=dict(n_iters=ITERS, loss_fn=fmpnp.geman_mcclure_loss, lambda_=0.01,
+                                            ratio_threshold=None))
+    pipe.run(batches)  # sizes the slab ring
+    best = None
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = pipe.run(batches)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return {"queries_per_s": round(nb * qb / best, 1), "ms_per_query": round(best / (nb * qb) * 1e3, 4),
+            "batches": nb, "batch": qb, "statuses": sorted({r["status"] for b in res for r in b}),
+            "note": "wall clock, host included: f-only pack and reference gather of every query (distinct maps) + "
+                    "one LM launch per batch, two streams"}
+
+
+def cpu_info():
+    model = ""
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    cpu_model = line.split(":", 1)[1].strip()
+                    model = line.split(":", 1)[1].strip()
                     break
     except OSError:
         pass
-    return {"value": round(args.cpu_sample / dt, 4), "unit": "pose-refinements/s", "cores": threads,
-            "kind": "port", "gn_iters_per_s": round(args.cpu_sample * ITERS / dt, 1),
-            "sample": f"{args.cpu_sample} cfg2 queries ({n_maps} distinct maps), 50 iters each, fp64 CHW "
-                      f"reference layout, {dt:.1f}s", "cpu": cpu_model}
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    return model, os.cpu_count(), affinity
+
+
+def cpu_baseline(args, res_gpu, synth, dev):
+    """CPU baselines on the GPU box's host, on queries the GPU refined in this run (global
+    indices 0..S-1, S distinct maps): (1) the C restatement of the reference loop
+    (oracle/fmpnp_oracle.c, OpenMP over queries) on every core of the job's CPU share;
+    (2) the vectorised PyTorch-CPU fp64 restatement (oracle/ref_torch.py) at 1 thread and
+    at that core count.  Both sides' poses are compared with the GPU's."""
+    import oracle.oracle as orc
+    from oracle import ref_torch
+    model, ncpu, affinity = cpu_info()
+    # the job's share of the host (OMP_NUM_THREADS: 16 per GPU on the pool's boxes)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
+    threads = args.cpu_threads or max(1, min(share, affinity))
+    S = min(len(res_gpu), max(2 * threads, 16))
+    maps = []
+    for q in range(S):
+        # the GPU run's own inputs (device generator), copied to the host in fp64 (exact)
+        inp = synth.problem_inputs(N_PTS, C, HF, WF, seed=q, device=dev, init=args.init)
+        fm = inp.pop("fmap").double().cpu().numpy()
+        inp["fref"] = inp["fref"].double().cpu().numpy()
+        gx, gy = orc.sobel(fm)
+        maps.append((inp, fm, gx, gy))
+    probs = [orc.make_problem(inp["pts3d"], inp["fref"], fm, gx, gy, inp["K"], inp["im_width"],
+                              inp["im_height"], inp["R0"], inp["t0"]) for inp, fm, gx, gy in maps]
+    copts = orc.make_options(ITERS, 0.01, "geman_mcclure", args.ratio)
+    orc.lib()
+    n_sample = max(S, args.cpu_sample)
+    sample = [probs[i % S] for i in range(n_sample)]
+    t = time.perf_counter()
+    cres = orc.forward_batch(sample, copts, threads)
+    dt = time.perf_counter() - t
+
+    def cmp(poses):
+        rot = max(rot_angle(p[0], g["R"]) for p, g in zip(poses, res_gpu))
+        tr = max(float(np.linalg.norm(np.asarray(p[1]) - g["t"])) for p, g in zip(poses, res_gpu))
+        return {"queries_compared": len(poses), "max_rot_diff_rad": rot, "max_t_diff_m": tr,
+                "within_1e-4": bool(rot < 1e-4 and tr < 1e-4)}
+    c_cmp = cmp([(r["R"], r["t"]) for r in cres[:S]])
+    out = {"value": round(n_sample / dt, 4), "unit": "pose-refinements/s", "cores": threads, "kind": "port",
+           "gn_iters_per_s": round(n_sample * ITERS / dt, 1),
+           "sample": f"{n_sample} cfg2 problems = {S} distinct queries (global indices 0..{S - 1}, own map each) "
+                     f"repeated, 50 iters, GM, fp64 CHW maps, C restatement, OpenMP {threads} threads, {dt:.1f}s",
+           "cpu": model, "nproc": ncpu, "affinity_cpus": affinity, "job_cpu_share": share,
+           "poses_vs_gpu": c_cmp}
+    if not c_cmp["within_1e-4"]:
+        log("[bench] WARNING: CPU (C oracle) and GPU poses differ by more than 1e-4", c_cmp)
+    # the vectorised PyTorch-CPU fp64 restatement, 1 thread and the job's share
+    tt = {}
+    prev_threads = torch.get_num_threads()
+    for nth, nq in ((1, 4), (threads, 2 * threads)):
+        torch.set_num_threads(nth)
+        nq = min(nq, S)
+        poses = []
+        t = time.perf_counter()
+        for q in range(nq):
+            inp, fm, gx, gy = maps[q]
+            R, tv, _ = ref_torch.forward(inp["pts3d"], inp["fref"], fm, gx, gy, inp["K"], inp["im_width"],
+                                         inp["im_height"], inp["R0"], inp["t0"], ITERS, 0.01, "geman_mcclure",
+                                         args.ratio)
+            poses.append((R.numpy(), tv.numpy()))
+        dt = time.perf_counter() - t
+        tt[f"threads_{nth}"] = {"value": round(nq / dt, 4), "unit": "pose-refinements/s", "cores": nth,
+                                "sample": f"{nq} distinct cfg2 queries, 50 iters, {dt:.1f}s",
+                                "poses_vs_gpu": cmp(poses)}
+    torch.set_num_threads(prev_threads)
+    out["pytorch_cpu_fp64"] = tt
+    return out
 
 
 if __name__ == "__main__":

@@ -5,6 +5,8 @@ Queries are independent, so a batch is cut into contiguous blocks, one per rank
 run.py:38-39).  No collective touches the data path; the only exchange is the
 optional final gather of the small per-query results (12 doubles + counters).
 """
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -15,6 +17,37 @@ def shard_range(n_total, rank, world):
     lo = rank * base + min(rank, extra)
     hi = lo + base + (1 if rank < extra else 0)
     return lo, hi
+
+
+def query_indices(rank, world, per_rank=0, global_batch=0):
+    """Global indices of this rank's queries.  Strong scaling (global_batch > 0): a fixed total
+    split into contiguous blocks; weak scaling: per_rank queries per rank, i.e. the blocks of
+    per_rank * world.  The index is the query's identity everywhere (bench.py seeds its
+    synthetic inputs with it), so any rank count refines the same queries."""
+    n_total = int(global_batch) if global_batch > 0 else int(per_rank) * int(world)
+    return range(*shard_range(n_total, rank, world))
+
+
+def timed_steps(step, steps, device=None, group=None):
+    """Run step(k) for k < steps between two barrier + device-synchronise fences; returns the
+    elapsed wall seconds, maximised over ranks (the slowest rank sets the job's time)."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+
+    def fence():
+        if world > 1:
+            dist.barrier(group)
+        if device is not None:
+            torch.cuda.synchronize(device)
+
+    fence()
+    t0 = time.perf_counter()
+    for k in range(int(steps)):
+        step(k)
+    if device is not None:
+        torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    fence()
+    return max_over_ranks(elapsed, device=device, group=group)
 
 
 def refine_sharded(make_problem, n_total, refine_fn, group=None):

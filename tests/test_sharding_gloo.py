@@ -2,7 +2,10 @@
 
 The compute of each shard here is the CPU oracle (test infrastructure) standing in
 for the device refiner: this test covers the distribution plumbing -- contiguous
-blocks, all-gather in global order, max-over-ranks timing -- not the kernel.
+blocks, all-gather in global order, max-over-ranks timing -- not the kernel.  The
+functions are the ones bench.py runs on N GPUs: fmpnp.shard.query_indices picks a
+rank's queries (their global index seeds their inputs) and fmpnp.shard.timed_steps
+brackets the timed launches.
 """
 import os
 import socket
@@ -11,7 +14,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from fmpnp.shard import shard_range
+from fmpnp.shard import query_indices, shard_range
 
 
 def test_shard_range_covers_all():
@@ -23,6 +26,18 @@ def test_shard_range_covers_all():
                 assert b == c
             sizes = [b - a for a, b in blocks]
             assert max(sizes) - min(sizes) <= 1
+
+
+def test_query_indices_weak_and_strong():
+    # weak scaling: B per rank, blocks of the global index space; strong: a fixed total split
+    for world in (1, 2, 4, 8):
+        weak = [list(query_indices(r, world, per_rank=128)) for r in range(world)]
+        assert sum(weak, []) == list(range(128 * world))
+        strong = [list(query_indices(r, world, global_batch=1024)) for r in range(world)]
+        assert sum(strong, []) == list(range(1024))
+        assert all(len(b) == 1024 // world for b in strong)
+    # the rank-0 share of the weak form is the same queries at every world size
+    assert list(query_indices(0, 8, per_rank=128)) == list(query_indices(0, 1, per_rank=128))
 
 
 def _problem(i):
@@ -49,12 +64,19 @@ def _worker(rank, world, port, n, q):
     sys.path[:0] = [root, os.path.join(root, "featuremetric-pnp_amd"), os.path.join(root, "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
-    from fmpnp.shard import max_over_ranks, refine_sharded
+    import time
+    from fmpnp.shard import max_over_ranks, query_indices, refine_sharded, timed_steps
     dist.init_process_group("gloo", rank=rank, world_size=world)
     res = refine_sharded(_problem, n, _refine)
     m = max_over_ranks(float(rank + 1))
+    # bench.py's timed region: rank 1 is slower; every rank reports the slowest rank's time
+    steps = []
+    el = timed_steps(lambda k: (steps.append(k), time.sleep(0.05 * (rank + 1))), 3)
+    mine = list(query_indices(rank, world, per_rank=3))
+    got = [None] * world
+    dist.all_gather_object(got, (el, steps, mine))
     if rank == 0:
-        q.put((res, m))
+        q.put((res, m, got))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -76,12 +98,16 @@ def test_two_rank_gloo_matches_single_process():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res, m = q.get(timeout=200)
+    res, m, got = q.get(timeout=200)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     single = _refine([_problem(i) for i in range(n)])
     assert m == 2.0
+    (el0, st0, q0), (el1, st1, q1) = got
+    assert el0 == el1 and el0 >= 0.3  # max over ranks: rank 1's 3 x 0.1 s
+    assert st0 == st1 == [0, 1, 2]
+    assert q0 == [0, 1, 2] and q1 == [3, 4, 5]
     assert len(res) == n
     for a, b in zip(res, single):
         assert a["R"] == b["R"] and a["t"] == b["t"] and a["best_cost"] == b["best_cost"]

@@ -6,9 +6,9 @@ FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB.  On gfx950 FETCH_
 reports half of the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM section):
 it is doubled here; WRITE_SIZE is taken as is.
 
-usage: pmc_summary.py <prof_dir> <batch> <out.json> [kernel name substring]
-(default: the benchmarked variant, lm_kernel<float, 2, false, false, 1>: fp32 texels, one
-workgroup per problem, no ratio test, Geman-McClure on the packed f/gx/gy layout)
+usage: pmc_summary.py <prof_dir> <batch> <out.json> [kernel name substring | auto] [tag]
+(default "auto": the lm_kernel variant with the largest total time in the kernel trace --
+the workload's LM launch, whichever specialisation the planner picked)
 """
 import csv
 import glob
@@ -38,12 +38,18 @@ def counter_avg(prof, sub, name, kernel_key):
 
 def main():
     prof, batch, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
-    key = sys.argv[4] if len(sys.argv) > 4 else "lm_kernel<float, 2, false, false, 1>"
+    key = sys.argv[4] if len(sys.argv) > 4 else "auto"
+    tag = sys.argv[5] if len(sys.argv) > 5 else None
     stats = [r for r in rows(os.path.join(prof, "trace", "**", "*kernel_stats.csv"))]
+    if key == "auto":
+        lms = [r for r in stats if "lm_kernel" in r.get("Name", "")]
+        lms.sort(key=lambda r: float(r.get("TotalDurationNs") or 0), reverse=True)
+        key = lms[0]["Name"].replace("void ", "").split("(")[0] if lms else "lm_kernel"
     lm = [r for r in stats if key in r.get("Name", "")]
     fetch_kib, nf = counter_avg(prof, "pmc_fetch", "FETCH_SIZE", key)
     write_kib, nw = counter_avg(prof, "pmc_write", "WRITE_SIZE", key)
     summary = {
+        "tag": tag,
         "batch": batch,
         "kernel": lm[0]["Name"] if lm else None,
         "kernel_calls": int(lm[0]["Calls"]) if lm else None,
