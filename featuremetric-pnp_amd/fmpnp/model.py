@@ -184,12 +184,13 @@ class sparseFeaturePnP(nn.Module):
                 R, t = self._forward_packed(feats, pts3D, fref_t, K, im_width, im_height, R, t, track,
                                             c_begin=start, c_end=end_c)
                 continue
-            # resized / blurred level (model.py:196-207): device resize, optional Gaussian, device Sobel
-            lvl = fm[start:end_c].to(self._device(fm), dtype=feats.dtype)[None]
+            # resized / blurred level (model.py:196-207): device resize and Gaussian in fp64 (the
+            # reference's maps are fp64 here, optimize_feature_pnp.py:57), then the device Sobel + pack
+            lvl = fm[start:end_c].to(feats.buf.device, dtype=torch.float64)[None]
             if target_size is not None:
                 lvl = nn.functional.interpolate(lvl, size=(target_size, target_size), mode="bilinear")
             if kernel_size is not None:
-                lvl = _gaussian_blur(lvl, kernel_size)
+                lvl = gaussian_blur(lvl, kernel_size, groups=end - start)
             lf = _rf.pack_features(lvl[0], storage=feats.dtype, device=feats.buf.device)
             R, t = self._forward_packed(lf, pts3D, fref_t[:, start:end_c], K, im_width, im_height, R, t, track)
         return R, t
@@ -240,15 +241,34 @@ def _find_inliers_packed(feats, pts3D, R, t, feature_ref, K, im_width, im_height
     return mask.cpu()
 
 
-def _gaussian_blur(x, kernel_size, sigma=1.0):
-    """kornia.filters.get_gaussian_kernel2d((k,k),(1,1)) + grouped conv2d padding=1 (model.py:199-200).
-    Parity unpinned: kornia 0.2.2 is not available to check against."""
-    k = kernel_size
-    xs = torch.arange(k, dtype=x.dtype, device=x.device) - (k - 1) / 2.0
-    g = torch.exp(-(xs ** 2) / (2.0 * sigma ** 2))
+def gaussian_kernel2d(kernel_size, sigma=1.0):
+    """kornia.filters.get_gaussian_kernel2d((k, k), (sigma, sigma)) as kornia 0.2.2 publishes it
+    (requirements.txt:5): the 1-D window exp(-(i - k//2)^2 / (2 sigma^2)), i < k, in fp32,
+    normalised by its fp32 sum, and the 2-D kernel as the fp32 outer product of the two
+    windows.  An even or non-positive size raises TypeError, as kornia's
+    get_gaussian_kernel1d does.  Parity unpinned: kornia is not importable here."""
+    if not isinstance(kernel_size, int) or kernel_size <= 0 or kernel_size % 2 == 0:
+        raise TypeError(f"kernel_size must be an odd positive integer. Got {kernel_size}")
+    x = torch.arange(kernel_size, dtype=torch.float32) - kernel_size // 2
+    g = torch.exp(-x.pow(2.0) / float(2 * sigma ** 2))
     g = g / g.sum()
-    ker = torch.outer(g, g)[None, None].repeat(x.shape[1], 1, 1, 1)
-    return nn.functional.conv2d(x, ker, groups=x.shape[1], padding=1)
+    return torch.matmul(g.unsqueeze(-1), g.unsqueeze(-1).t())
+
+
+def gaussian_blur(x, kernel_size, groups=None):
+    """The blurred pyramid level of model.py:199-200: the fp32 kernel repeated `groups`
+    (= end - start) times, as fp64, grouped conv2d with padding=1 (same size only for k=3;
+    the reference keeps padding=1 for every k).  x: [1, C_level, H, W] fp64.  Like the
+    reference, a level whose channel slice was clamped by Python slicing (end > C) has
+    fewer channels than groups and raises RuntimeError."""
+    groups = x.shape[1] if groups is None else int(groups)
+    ker = gaussian_kernel2d(kernel_size)[None, None].repeat(groups, 1, 1, 1).to(device=x.device,
+                                                                                 dtype=torch.float64)
+    if x.shape[1] != groups:
+        raise RuntimeError(f"Given groups={groups}, weight of size {list(ker.shape)}, expected input "
+                           f"{list(x.shape)} to have {groups} channels, but got {x.shape[1]} channels instead "
+                           "(model.py:199-200 with a pyramid level whose end exceeds the channel count)")
+    return nn.functional.conv2d(x.to(torch.float64), ker, groups=groups, padding=1)
 
 
 def is_nan(x):
