@@ -50,7 +50,8 @@ import torch  # noqa: E402
 N_PTS, C, HF, WF, ITERS = 512, 256, 240, 320, 50
 HBM_PEAK = 8.0e12  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 B_ITER = N_PTS * (16 * C + 24)  # SURVEY.md §8d bytes per GN iteration per query (every point re-read)
-LEGS = ["single", "hard", "ratio", "no_memo", "bilinear", "layout_f", "pack", "pipeline", "fixed1024", "cpu"]
+LEGS = ["single", "hard", "ratio", "no_spec", "no_memo", "bilinear", "layout_f", "pack", "pipeline", "fixed1024",
+        "cpu"]
 
 
 def parse():
@@ -309,6 +310,10 @@ def run_legs(args, dev, probs, feats, inputs, opts, res_main, rf, _lib, synth):
         out["ratio08"] = leg_summary(workload_tag(B, args.init, 0.8, memo, args.sampling, args.layout), ms, r, B,
                                      args.sampling, args.layout)
         out["ratio08"]["kernel_variant"] = "RATIO=true"
+    if "no_spec" in args.legs and memo:  # memoised, without the speculative next-texel gathers
+        ms, r = time_launches(rf.AsyncBatch(probs, opt(speculate=False)), 10, stream)
+        out["no_spec"] = leg_summary(workload_tag(B, args.init, args.ratio, memo, args.sampling, args.layout) +
+                                     "_nospec", ms, r, B, args.sampling, args.layout, base=res_main)
     if "no_memo" in args.legs and memo:  # the reference's data movement: every texel re-read
         ms, r = time_launches(rf.AsyncBatch(probs, opt(memoize=False)), 5, stream)
         out["no_memo"] = leg_summary(workload_tag(B, args.init, args.ratio, False, args.sampling, args.layout), ms,

@@ -22,7 +22,7 @@ namespace {
 
 struct Plan {
     int G = 1, teams = 1, teams_pad = 8, gw = 8, grid = 8, nc_max = 1, max_n = 0;
-    int mmax = 0, lds = 0, wps = WPS_LATENCY;
+    int mmax = 0, lds = 0, wps = WPS_LATENCY, spec = 0;
     size_t ws_counters = 0, ws_partials = 0, ws_max = 0, ws_total = 0;
 };
 
@@ -59,6 +59,7 @@ int validate(const fmpnp_problem *probs, int n, const fmpnp_options *opt) {
     if (opt->layout == FMPNP_LAYOUT_F && (opt->dtype != FMPNP_F32 || opt->sampling != FMPNP_NEAREST))
         return FMPNP_EINVAL;
     if (opt->sobel_flags & ~3) return FMPNP_EINVAL;
+    if (opt->no_memo < 0 || opt->no_memo > 2) return FMPNP_EINVAL;
     for (int i = 0; i < n; ++i) {
         const int rc = validate_problem(probs[i], opt->layout);
         if (rc) return rc;
@@ -85,9 +86,12 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     rc = device_cus(&ncu);
     if (rc) return rc;
     const int lds_cu = 160 * 1024;  // LDS per CU
+    // speculative next-texel gathers (fmpnp_lm_impl.h spec_pass): memoised nearest sampling of
+    // a forward run; no_memo = 2 keeps the memo without them (a measurement knob)
+    P.spec = (opt->no_memo == 0 && opt->sampling == FMPNP_NEAREST && opt->mode == FMPNP_MODE_FORWARD) ? 1 : 0;
     auto lds_for = [&](int G) {
         const int m = ((P.nc_max + G - 1) / G) * CH;
-        return lds_fixed_bytes() + (int)lm_dyn_lds_bytes(m, P.nc_max);
+        return lds_fixed_bytes() + (int)lm_dyn_lds_bytes(m, P.nc_max, P.spec != 0);
     };
     // resident workgroups per CU (VGPR and LDS limits).  Hardware admission of 256-thread
     // blocks is also bounded by SGPRs: floor(800 / (ceil(sgpr/16)*16 + 16)) >= 6 for any
@@ -98,7 +102,7 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb,
                                                          lm_kernel_ptr(opt->dtype, P.wps, P.G > 1,
                                                                        opt->use_ratio != 0, lm_variant(*opt)),
-                                                         NT, lds) !=
+                                                         P.wps == WPS_THROUGHPUT ? NT_THROUGHPUT : NT, lds) !=
             hipSuccess)
             return 1;
         return std::max(1, std::min(nb, 6));
@@ -114,7 +118,7 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     } else {
         // (no_memo and bilinear sampling re-read every texel each evaluation: bandwidth-bound,
         // so every CU gets a workgroup; bilinear B=128: G=2 7.32 ms vs G=1 7.75 ms)
-        const bool streaming = opt->no_memo || opt->sampling == FMPNP_BILINEAR;
+        const bool streaming = opt->no_memo == 1 || opt->sampling == FMPNP_BILINEAR;
         G = (n <= 0 || (2L * n >= ncu && !streaming)) ? 1 : (ncu + n - 1) / n;
         // memoised packed-gradient loop on problems of <= 512 points: the evaluation is a
         // latency chain and a member's exchange costs about what the split saves, so one
@@ -131,13 +135,20 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     P.G = G;
     P.mmax = ((P.nc_max + G - 1) / G) * CH;
     P.lds = lds_for(G);
-    // occupancy variant: the 128-VGPR two-workgroups-per-CU build (WPS_THROUGHPUT) spills
-    // since the kernel went register-resident (73-106 VGPRs to scratch) and measured slower
-    // than running the latency build in rounds (B=512: 0.93 ms vs 2 x 0.42 ms), so the
-    // planner uses it only on request (FMPNP_LM_WPS=4, a tuning knob)
+    // build: with at least two problems per CU the throughput build (256-thread workgroups,
+    // two per CU: one problem's LM tail overlaps the other's point work) -- one workgroup per
+    // problem, no speculation (its LDS would not leave room for two workgroups, and with every
+    // CU busy there is no idle memory time to hide it in).  FMPNP_LM_WPS=2|4 forces a build.
     const char *wps_env = getenv("FMPNP_LM_WPS");
-    const bool want_tp = wps_env && atoi(wps_env) == 4;
-    P.wps = (want_tp && opt->layout == FMPNP_LAYOUT_FGRAD && G == 1 && (long)n >= 2L * ncu && 2 * P.lds <= lds_cu) ? WPS_THROUGHPUT : WPS_LATENCY;
+    const int want = wps_env ? atoi(wps_env) : 0;
+    const bool tp_ok = opt->layout == FMPNP_LAYOUT_FGRAD && G == 1 && (long)n >= ncu &&
+                       2 * (lds_fixed_bytes() + (int)lm_dyn_lds_bytes(P.mmax, P.nc_max, false)) <= lds_cu;
+    const bool tp = tp_ok && (want == WPS_THROUGHPUT || (want == 0 && (long)n >= 2L * ncu));
+    P.wps = tp ? WPS_THROUGHPUT : WPS_LATENCY;
+    if (tp) {
+        P.spec = 0;
+        P.lds = lds_for(G);
+    }
     const int per_cu = occupancy(P.lds);
     long cap = (long)ncu * per_cu;
     if (G == 1) cap = std::max(cap, (long)n);  // no cross-workgroup waits: any grid is safe
@@ -341,6 +352,11 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
     a.mmax = P.mmax;
     a.stamps = g_stamps;
     a.wps = P.wps;
+    a.spec = P.spec;
+    {
+        static const int dbg = [] { const char *e = getenv("FMPNP_DBG"); return e ? atoi(e) : 0; }();
+        a.dbg = dbg;
+    }
     hipError_t e = hipMemsetAsync(a.counters, 0, P.ws_counters, s);
     if (e != hipSuccess) return (int)e;
     e = hipMemsetAsync(results_dev, 0, sizeof(fmpnp_result) * (size_t)n, s);  // texel_gathers accumulate

@@ -10,13 +10,15 @@ namespace fmpnp {
 constexpr int NT = 512;         // threads per workgroup of the LM kernel (8 waves)
 constexpr int CH = 64;          // points per reduction chunk = one wave block (fixed: results do not depend on G)
 constexpr int NV = 32;          // reduced vector: 21 H + 6 g + rho + kept + supported + 2 pad
-constexpr int NSTAMP = 12;      // debug phase-stamp slots: 8 phases + eval-0 proj/gather/loss/contrib
+constexpr int NSTAMP = 13;      // debug phase-stamp slots: 8 phases + eval-0 proj/gather/loss/contrib + wave 0 speculation
 constexpr int RECW = 8;         // per-point record: 6 channel sums + rho + rho'
 constexpr int MAX_G = 64;       // workgroups per problem
-// LM kernel occupancy variants (waves per SIMD in __launch_bounds__): 2 = one 512-thread
-// workgroup per CU with up to 256 VGPRs (latency); 4 = two per CU within 128 VGPRs, so one
-// problem's serial LM tail overlaps another's point work (throughput, batches >= 2 x CUs)
+// LM kernel builds: WPS_LATENCY = one 512-thread workgroup (8 waves) per problem and per CU;
+// WPS_THROUGHPUT = 256-thread workgroups (4 waves, two 64-point blocks per wave at N=512),
+// two resident per CU, so one problem's serial LM tail overlaps the other's point work
+// (batches of >= 2 problems per CU).  Both keep 2 waves per SIMD: up to 256 VGPRs.
 constexpr int WPS_LATENCY = 2, WPS_THROUGHPUT = 4;
+constexpr int NT_THROUGHPUT = 256;
 
 // Kernel arguments (by value).
 struct LaunchArgs {
@@ -33,6 +35,8 @@ struct LaunchArgs {
     int mmax;                     // max points per workgroup (multiple of CH): dynamic LDS carve
     unsigned long long *stamps;   // debug: [grid][8 waves][NSTAMP] phase cycle totals, or null
     int wps;                      // occupancy variant (WPS_LATENCY / WPS_THROUGHPUT)
+    int spec;                     // speculative next-texel gathers (memoised nearest modes)
+    int dbg;                      // debug knob (FMPNP_DBG): bit 0 census only, bit 1 no consume
 };
 
 // Fixed LDS head: the LM state + per-problem context (sized generously, 16-B aligned).
@@ -40,7 +44,12 @@ __host__ __device__ constexpr int lds_fixed_bytes() { return 4096; }
 // row stride (doubles) of the LM kernel's structure-of-arrays LDS records: odd, so the
 // writers of one point's fields fall in distinct banks (fmpnp_lm_impl.h lds_X / lds_rec)
 __host__ __device__ constexpr int lds_rs(int mmax) { return mmax + 1; }
-size_t lm_dyn_lds_bytes(int mmax, int nc_max);
+// speculative next-texel records (fmpnp_lm_impl.h lds_rec2 ...): rec2[6][rs] doubles, and
+// 32-bit words for tex, tex2, spec, slot, qp[2] per point (16-B padded); without speculation
+// only tex
+__host__ __device__ constexpr int lds_spec_doubles(int mmax, bool spec) { return spec ? 6 * lds_rs(mmax) : 0; }
+__host__ __device__ constexpr int lds_words(int mmax, bool spec) { return ((spec ? 6 : 1) * mmax + 3) / 4 * 4; }
+size_t lm_dyn_lds_bytes(int mmax, int nc_max, bool spec);
 
 hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream);
 // LM kernel variants (fmpnp_lm_impl.h): Geman-McClure forward with nearest sampling (the

@@ -59,14 +59,15 @@ int lm_variant(const fmpnp_options &o) {
 hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream) {
     typedef void (*LmFn)(LaunchArgs);
     const LmFn f = (LmFn)lm_kernel_ptr(dtype, a.wps, a.G > 1, a.opt.use_ratio != 0, lm_variant(a.opt));
-    hipLaunchKernelGGL(f, dim3(grid), dim3(NT), lds, stream, a);
+    hipLaunchKernelGGL(f, dim3(grid), dim3(a.wps == WPS_THROUGHPUT ? NT_THROUGHPUT : NT), lds, stream, a);
     return hipGetLastError();
 }
 
-size_t lm_dyn_lds_bytes(int mmax, int nc_max) {
-    // X[3][rs] + rec[RECW][rs] doubles (rs = mmax + 1), tex[M] ints (16-B padded),
-    // part[nc_max][NV] doubles
-    return (size_t)(3 + RECW) * lds_rs(mmax) * 8 + (size_t)((mmax + 3) / 4) * 16 + (size_t)nc_max * NV * 8;
+size_t lm_dyn_lds_bytes(int mmax, int nc_max, bool spec) {
+    // X[3][rs] + rec[RECW][rs] (+ rec2[6][rs]) doubles (rs = mmax + 1), 32-bit per-point words
+    // (tex; + tex2, spec, qp[2] with speculation; 16-B padded), part[nc_max][NV] doubles
+    return ((size_t)(3 + RECW) * lds_rs(mmax) + lds_spec_doubles(mmax, spec)) * 8 + (size_t)lds_words(mmax, spec) * 4 +
+           (size_t)nc_max * NV * 8;
 }
 
 }  // namespace fmpnp

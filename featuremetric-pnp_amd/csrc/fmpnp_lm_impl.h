@@ -60,6 +60,8 @@ struct Ctx {
     double *max_g;        // [2][G] of this team
     double lambda0, ratio_thr, alpha;
     int mode, n_iters, use_ratio, loss, G, s, trace_stride, nc_max, no_memo, sampling, sobel_flags;
+    int spec;             // speculative gathers of the predicted next texels (memoised nearest modes)
+    int dbg;
     unsigned epoch;       // exchanges done by this team in this launch
     int dead;             // a team exchange timed out: finish remaining problems as failed
     int stamps_on;        // debug phase stamps enabled
@@ -82,6 +84,9 @@ struct PC {
     int Hf, Wf, cs, cb, ce, ld, im_w, im_h, p0, M, c0, LC, G;
     UDiv dh, dw;
     int loss, no_memo, use_ratio, bilinear;
+    int spec;               // speculative next-texel gathers on (runtime: launch option)
+    int dbg;
+    float txpx, typx, pxtx, pypx;  // texels per image pixel and image pixels per texel (x, y)
     int sob_norm, sob_rep;  // FMPNP_LAYOUT_F: the in-gather Sobel's flags
     double alpha;
     double *part_g;       // this team's partial slots [2][nc_max][NV] (G > 1)
@@ -90,6 +95,9 @@ struct PC {
 };
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// waves of this workgroup: 8 (NT threads, the latency build) or 4 (the throughput build's
+// 256-thread workgroups, two per CU)
+__device__ __forceinline__ int nwaves() { return (int)(blockDim.x >> 6); }
 __device__ __forceinline__ unsigned ufirst(unsigned v) { return (unsigned)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ double ufirst(double v) {
     const long long b = __double_as_longlong(v);
@@ -135,6 +143,12 @@ __device__ __forceinline__ PC load_pc() {
     q.dw = UDiv{ufirst(c.div_w.m), ufirst(c.div_w.s1), ufirst(c.div_w.s2)};
     q.loss = ufirst(c.mode == FMPNP_MODE_COMPUTE_COST ? (int)FMPNP_SQUARED : c.loss);
     q.no_memo = ufirst(c.no_memo);
+    q.spec = ufirst(c.spec);
+    q.dbg = ufirst(c.dbg);
+    q.txpx = (float)q.Wf / (float)q.im_w;
+    q.typx = (float)q.Hf / (float)q.im_h;
+    q.pxtx = (float)q.im_w / (float)q.Wf;
+    q.pypx = (float)q.im_h / (float)q.Hf;
     q.bilinear = ufirst(c.sampling == FMPNP_BILINEAR ? 1 : 0);
     q.use_ratio = ufirst(c.use_ratio);
     q.alpha = ufirst(c.alpha);
@@ -163,13 +177,27 @@ __device__ __forceinline__ unsigned char *dyn() { return lm_lds + lds_fixed_byte
 // A lane-per-point read of coordinate / record field k (X[k][i], rec[k][i]) is 64 consecutive
 // doubles: conflict-free.  A gather's six writers (field e6 of one point j) hit banks
 // 2 (e6 rs + j) mod 64, distinct because rs is odd.
+//   speculation (lds_spec_doubles / lds_words: only tex when it is off): a second record slot
+//   rec2[6][rs] doubles, then after tex: tex2[mmax] (the texel of the slot not in use),
+//   spec[mmax] (this evaluation's prediction), slot[mmax] (the slot in use: 0 rec, 1 rec2),
+//   qp[2][mmax] floats (the last projected pixel position)
 __device__ __forceinline__ double *lds_X(int mmax) { return reinterpret_cast<double *>(dyn()); }
 __device__ __forceinline__ double *lds_rec(int mmax) { return reinterpret_cast<double *>(dyn()) + 3 * lds_rs(mmax); }
-__device__ __forceinline__ int *lds_tex(int mmax) {
-    return reinterpret_cast<int *>(reinterpret_cast<double *>(dyn()) + (3 + RECW) * lds_rs(mmax));
+__device__ __forceinline__ double *lds_rec2(int mmax) {
+    return reinterpret_cast<double *>(dyn()) + (3 + RECW) * lds_rs(mmax);
 }
-__device__ __forceinline__ double *lds_part(int mmax) {
-    return reinterpret_cast<double *>(dyn()) + (3 + RECW) * lds_rs(mmax) + ((mmax + 3) / 4) * 2;
+__device__ __forceinline__ int *lds_tex(int mmax, bool spec) {
+    return reinterpret_cast<int *>(reinterpret_cast<double *>(dyn()) + (3 + RECW) * lds_rs(mmax) +
+                                   lds_spec_doubles(mmax, spec));
+}
+__device__ __forceinline__ int *lds_tex2(int mmax, bool spec) { return lds_tex(mmax, spec) + mmax; }
+__device__ __forceinline__ int *lds_spec(int mmax, bool spec) { return lds_tex(mmax, spec) + 2 * mmax; }
+__device__ __forceinline__ int *lds_slot(int mmax, bool spec) { return lds_tex(mmax, spec) + 3 * mmax; }
+__device__ __forceinline__ float *lds_qp(int mmax, bool spec) {
+    return reinterpret_cast<float *>(lds_tex(mmax, spec) + 4 * mmax);
+}
+__device__ __forceinline__ double *lds_part(int mmax, bool spec) {
+    return reinterpret_cast<double *>(lds_tex(mmax, spec) + lds_words(mmax, spec));
 }
 
 // so3exp_map (helpers/utils.py:209-221) and the update R' = dR R, t' = dR t + dt
@@ -314,9 +342,20 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
     double *X = lds_X(mmax);
     const double *src = c.pts + 3 * (size_t)c.p0;
     const int rs = lds_rs(mmax);
-    for (int e = tid; e < 3 * c.M; e += NT) X[(e % 3) * rs + e / 3] = src[e];
-    int *tex = lds_tex(mmax);
-    for (int i = tid; i < mmax; i += NT) tex[i] = -2;  // no texel cached yet
+    const int nt = (int)blockDim.x;
+    for (int e = tid; e < 3 * c.M; e += nt) X[(e % 3) * rs + e / 3] = src[e];
+    int *tex = lds_tex(mmax, c.spec);
+    for (int i = tid; i < mmax; i += nt) tex[i] = -2;  // no texel cached yet
+    if (c.spec) {
+        int *tex2 = lds_tex2(mmax, true), *slot = lds_slot(mmax, true), *spec = lds_spec(mmax, true);
+        float *qp = lds_qp(mmax, true);
+        for (int i = tid; i < mmax; i += nt) {
+            tex2[i] = -2;
+            slot[i] = 0;
+            spec[i] = -1;
+            qp[i] = qp[mmax + i] = __builtin_nanf("");  // no motion known: no prediction at evaluation 0
+        }
+    }
     __syncthreads();
 }
 
@@ -512,7 +551,7 @@ __device__ __forceinline__ bool ratio_exchange(double lmax) {
     __syncthreads();
     if (tid == 0) {
         double m = st.wg_max[0];
-        for (int w = 1; w < NT / 64; ++w) m = nanmax(m, st.wg_max[w]);
+        for (int w = 1; w < nwaves(); ++w) m = nanmax(m, st.wg_max[w]);
         st.rho_max = m;
         if (c.G > 1) st_sc1(c.max_g + ((c.epoch + 1) & 1) * c.G + c.s, m);
     }
@@ -593,7 +632,7 @@ __device__ __forceinline__ void contrib_block(const PC &q, int mmax, int blk, bo
     const double tot = reduce32_in64(val, lane);
     if (lc < q.LC && (lane & 1) == 0) {
         const int idx = reduce32_index(lane);
-        if (q.G == 1) lds_part(mmax)[(size_t)(q.c0 + lc) * NV + idx] = tot;  // G == 1 (LDS)
+        if (q.G == 1) lds_part(mmax, q.spec)[(size_t)(q.c0 + lc) * NV + idx] = tot;  // G == 1 (LDS)
         else st_sc1(dst_g + (size_t)(q.c0 + lc) * NV + idx, tot);
     }
 }
@@ -640,6 +679,17 @@ __device__ __forceinline__ void g_consume(const GLoad<T> &g, bool has1, bool has
              has2 ? (double)sy[k] : z);
     }
 }
+
+// Where a gathered point's record fields go: this lane's field column (e6) at the block start
+// in the two record slots.  A gather always fills the slot a point is NOT currently using
+// (its current slot keeps serving until the evaluation switches over): point j is written
+// into slot a when bit j of `sel` is set (its current slot is b), else into b.  a == b: one
+// slot (no speculation).
+struct RecDst {
+    double *a, *b;
+    unsigned long long sel;
+    __device__ __forceinline__ double *col(int j) const { return ((sel >> j) & 1ull) ? a : b; }
+};
 
 // Pair selection from a dirty mask: the half-waves take the two lowest set lanes.
 struct GPair {
@@ -712,7 +762,7 @@ __device__ __forceinline__ void gather_bil_half(const T *__restrict__ feat, cons
 template <typename T>
 __device__ __forceinline__ void gather_bil_block(unsigned long long m, const Taps &tp, bool hi, int lane,
                                                  const T *feat, const T *fref0, int cs, int cb, int ce, int ld,
-                                                 bool vec, double *rec0, bool wlane) {
+                                                 bool vec, const RecDst &rd, bool wlane) {
     const int l32 = lane & 31;
     while (m) {
         const int pa = __builtin_ctzll(m);
@@ -737,17 +787,17 @@ __device__ __forceinline__ void gather_bil_block(unsigned long long m, const Tap
         if (vec) gather_bil_half<T, true>(feat, o, w, rf, cs, cb, ce, l32, v);
         else gather_bil_half<T, false>(feat, o, w, rf, cs, cb, ce, l32, v);
         const double r = reduce8_in32(v, lane);
-        if (wlane && (!hi || two)) rec0[src] = r;
+        if (wlane && (!hi || two)) rd.col(src)[src] = r;
     }
 }
 
 // Double-buffered pair gathers of one block: the next pair's loads are issued before this
 // pair's channel sums are reduced (one exposed round trip per block, not one per pair).
-// fref0: the block's first descriptor row; rec0: this lane's record field (e6) at the block start.
+// fref0: the block's first descriptor row; rd: where the records go.
 template <typename T, bool FULL>
 __device__ __forceinline__ void gather_pipe(unsigned long long m, int off, bool hi, int lane, const T *feat,
                                             const T *fref0, int cs, int ld, int gc1, int gc2, bool has1, bool has2,
-                                            double *rec0, bool wlane) {
+                                            const RecDst &rd, bool wlane) {
     if (!m) return;
     GLoad<T> A, B;
     GPair pa = pick_pair(m, off, hi), pb;
@@ -762,7 +812,7 @@ __device__ __forceinline__ void gather_pipe(unsigned long long m, int off, bool 
             double v[8];
             g_consume<T, FULL>(A, has1, has2, v);
             const double r = reduce8_in32(v, lane);
-            if (wlane && (!hi || pa.two)) rec0[pa.j] = r;
+            if (wlane && (!hi || pa.two)) rd.col(pa.j)[pa.j] = r;
         }
         if (!moreB) break;
         const bool moreA = m != 0;
@@ -774,7 +824,7 @@ __device__ __forceinline__ void gather_pipe(unsigned long long m, int off, bool 
             double v[8];
             g_consume<T, FULL>(B, has1, has2, v);
             const double r = reduce8_in32(v, lane);
-            if (wlane && (!hi || pb.two)) rec0[pb.j] = r;
+            if (wlane && (!hi || pb.two)) rd.col(pb.j)[pb.j] = r;
         }
         if (!moreA) break;
     }
@@ -888,7 +938,7 @@ __device__ __forceinline__ void f_issue(FTrip<T> &tr, unsigned long long &m, int
 }
 
 template <typename T, bool FULL>
-__device__ __forceinline__ void f_consume(const FTrip<T> &tr, bool has, bool norm, int lane, double *rec0,
+__device__ __forceinline__ void f_consume(const FTrip<T> &tr, bool has, bool norm, int lane, const RecDst &rd,
                                           bool wlane) {
     constexpr int V = V16<T>::n;
     double a[8];
@@ -908,7 +958,7 @@ __device__ __forceinline__ void f_consume(const FTrip<T> &tr, bool has, bool nor
     double r = reduce8_in32(a, lane), r2 = r;
     swap32(r, r2);
     r = r + r2;
-    if (wlane && lane < 32) rec0[tr.p] = r;
+    if (wlane && lane < 32) rd.col(tr.p)[tr.p] = r;
 }
 
 // Double-buffered form for C <= 64 V with 16-byte loads (one channel round per lane): the
@@ -917,7 +967,7 @@ __device__ __forceinline__ void f_consume(const FTrip<T> &tr, bool has, bool nor
 template <typename T, bool FULL>
 __device__ __forceinline__ void gather_f_pipe(unsigned long long m, int rc, int lane, const T *feat, const T *fref0,
                                               int cs, int cb, int ce, int ld, int Hf, int Wf, bool norm, bool rep,
-                                              double *rec0, bool wlane) {
+                                              const RecDst &rd, bool wlane) {
     constexpr int V = V16<T>::n;
     if (!m) return;
     const int c0 = cb + lane * V;
@@ -928,11 +978,11 @@ __device__ __forceinline__ void gather_f_pipe(unsigned long long m, int rc, int 
     while (true) {
         const bool moreB = m != 0;
         if (moreB) f_issue<T>(B, m, rc, feat, fref0, cs, ld, c, Hf, Wf, rep);
-        f_consume<T, FULL>(A, has, norm, lane, rec0, wlane);
+        f_consume<T, FULL>(A, has, norm, lane, rd, wlane);
         if (!moreB) break;
         const bool moreA = m != 0;
         if (moreA) f_issue<T>(A, m, rc, feat, fref0, cs, ld, c, Hf, Wf, rep);
-        f_consume<T, FULL>(B, has, norm, lane, rec0, wlane);
+        f_consume<T, FULL>(B, has, norm, lane, rd, wlane);
         if (!moreA) break;
     }
 }
@@ -941,7 +991,7 @@ __device__ __forceinline__ void gather_f_pipe(unsigned long long m, int rc, int 
 template <typename T>
 __device__ __forceinline__ void gather_f_block(unsigned long long m, int rc, bool hi, int lane, const T *feat,
                                                const T *fref0, int cs, int cb, int ce, int ld, int Hf, int Wf,
-                                               bool vec, bool norm, bool rep, double *rec0, bool wlane) {
+                                               bool vec, bool norm, bool rep, const RecDst &rd, bool wlane) {
     while (m) {
         const int p = __builtin_ctzll(m);
         m &= m - 1;
@@ -968,7 +1018,207 @@ __device__ __forceinline__ void gather_f_block(unsigned long long m, int rc, boo
         double r = reduce8_in32(v, lane), r2 = r;
         swap32(r, r2);  // the two halves hold the point's even / odd channel groups
         r = r + r2;
-        if (wlane && !hi) rec0[p] = r;
+        if (wlane && !hi) rd.col(p)[p] = r;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The channel sums of the points of block `blk` set in the wave mask m, from the texels
+// `off` (lane-wise; FL: rc = (row << 16) | col), into the record columns recb (this lane's
+// field e6 at the block start: rec for the evaluation, rec2 for speculation).  Nearest
+// sampling: packed f/gx/gy or, FL, the f-only layout with the in-gather Sobel.
+// ---------------------------------------------------------------------------
+template <typename T, bool PIPE, bool FL>
+__device__ __forceinline__ void gather_records(const PC &q, unsigned long long m, int off, int rc, int blk,
+                                               const RecDst &rd, bool wlane) {
+    const int lane = threadIdx.x & 63, l32 = lane & 31;
+    const bool hi = lane >= 32;
+    const T *feat = reinterpret_cast<const T *>(q.feat);
+    const T *fref = reinterpret_cast<const T *>(q.fref);
+    const int cs = q.cs, cb = q.cb, ce = q.ce, p0 = q.p0, ld = q.ld;
+    constexpr int V = V16<T>::n;
+    const bool vec = ((((uintptr_t)feat) | ((uintptr_t)fref)) & 15) == 0 && cs % V == 0 && ld % V == 0 &&
+                     cb % V == 0 && (ce - cb) % V == 0;
+    const T *fref0 = fref + (size_t)(p0 + blk * 64) * ld;
+    if constexpr (FL) {
+        if (PIPE && vec && ce - cb <= 64 * V)  // one channel round per lane
+            gather_f_pipe<T, true>(m, rc, lane, feat, fref0, cs, cb, ce, ld, q.Hf, q.Wf, q.sob_norm != 0,
+                                   q.sob_rep != 0, rd, wlane);
+        else
+            gather_f_block<T>(m, rc, hi, lane, feat, fref0, cs, cb, ce, ld, q.Hf, q.Wf, vec, q.sob_norm != 0,
+                              q.sob_rep != 0, rd, wlane);
+    } else if (PIPE && vec && ce - cb <= 64 * V) {
+        // one round trip per point (every channel within the lane's two rounds), double-buffered
+        // pairs: the next pair's loads are issued before this pair's channel sums are reduced
+        // (one exposed round trip per block, not one per pair)
+        const int gc = cb + l32 * V;
+        const bool has1 = gc < ce, has2 = gc + 32 * V < ce;
+        const int gc1 = has1 ? gc : cb, gc2 = has2 ? gc + 32 * V : gc1;
+        if (ce - cb == 64 * V)
+            gather_pipe<T, true>(m, off, hi, lane, feat, fref0, cs, ld, gc1, gc2, has1, has2, rd, wlane);
+        else
+            gather_pipe<T, false>(m, off, hi, lane, feat, fref0, cs, ld, gc1, gc2, has1, has2, rd, wlane);
+    } else {
+        while (m) {  // wave-uniform: two dirty points per trip, one per half-wave
+            const GPair pp = pick_pair(m, off, hi);
+            const T *t = feat + (size_t)pp.to * 3 * cs;
+            const T *rf = fref0 + (size_t)pp.j * ld;
+            double v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = 0.0;
+            if (vec) gather_half<T, true>(t, rf, cs, cb, ce, l32, v);
+            else gather_half<T, false>(t, rf, cs, cb, ce, l32, v);
+            const double r = reduce8_in32(v, lane);
+            if (wlane && (!hi || pp.two)) rd.col(pp.j)[pp.j] = r;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Speculative next-texel gathers.  A point changes texel (and needs a gather) only when its
+// pixel crosses a texel edge, and -- measured over the reference's own LM trajectories at
+// the BASELINE shapes (tools/sim_spec.py) -- a point that crosses in the next evaluation
+// almost always lies closer to that edge, along each axis, than it moved in this one: the
+// predicted texel is the neighbour across the near edge of every such axis (97 % of the
+// next evaluation's dirty points, about two predictions per dirty point).  Waves 1..7 gather
+// the predicted texels' sums into rec2 while wave 0 runs the LM tail (the gathers leave the
+// evaluation's critical path); a dirty point whose new texel is rec2's takes its sums from
+// there -- the same gather code, so bit-identical records -- and only the mispredicted ones
+// are gathered in the evaluation itself.  Results do not depend on the predictions.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int spec_target(const PC &q, double qx, double qy, int row, int col, float *qpx,
+                                           float *qpy) {
+    const float fx = (float)qx, fy = (float)qy;
+    const float mx = fabsf(fx - *qpx), my = fabsf(fy - *qpy);  // NaN before the first motion: none
+    *qpx = fx;
+    *qpy = fy;
+    const float sx = (fx - 0.5f) * q.txpx, sy = (fy - 0.5f) * q.typx;  // continuous texel coordinates
+    const float ax = sx - floorf(sx), ay = sy - floorf(sy);
+    const bool cx = fminf(ax, 1.0f - ax) * q.pxtx < mx, cy = fminf(ay, 1.0f - ay) * q.pypx < my;
+    const int c2 = col + (cx ? (ax < 0.5f ? -1 : 1) : 0), r2 = row + (cy ? (ay < 0.5f ? -1 : 1) : 0);
+    return ((cx || cy) && c2 >= 0 && c2 < q.Wf && r2 >= 0 && r2 < q.Hf) ? r2 * q.Wf + c2 : -1;
+}
+
+// Every wave for its own blocks (wave 0 before the evaluation's barrier, in the slack it has
+// while the later waves of its SIMDs finish; waves 1..7 after it, beside wave 0's LM tail):
+// gather the predicted texels into each point's idle slot, which then holds tex2.
+template <typename T, bool PIPE, bool FL>
+__device__ __forceinline__ void spec_pass(const PC &q, int mmax, long long &ngath, int first_blk = -1) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int *tex = lds_tex(mmax, true), *spec = lds_spec(mmax, true), *slot = lds_slot(mmax, true);
+    const int *tex2 = lds_tex2(mmax, true);
+    double *rec = lds_rec(mmax), *rec2 = lds_rec2(mmax);
+    const int rs = lds_rs(mmax);
+    const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
+    const bool wlane = (lane & 3) == 0 && e6 < 6;
+    const size_t fo = (size_t)(wlane ? e6 : 0) * rs;
+    for (int blk = first_blk >= 0 ? first_blk : wave; blk * 64 < q.M; blk += nwaves()) {
+        const int i = blk * 64 + lane;
+        const bool valid = i < q.M;
+        const int ii = valid ? i : 0;
+        const int sp = valid ? spec[ii] : -1, cur = tex[ii], t2 = tex2[ii], sl = slot[ii];
+        const bool want = sp >= 0 && sp != cur && sp != t2;
+        const unsigned long long m = __ballot(want);
+        if (!m) continue;
+        ngath += __popcll(m);
+        int rc = 0;
+        if (FL && want) rc = ((sp / q.Wf) << 16) | (sp % q.Wf);
+        const RecDst rd{rec + fo + blk * 64, rec2 + fo + blk * 64, __ballot(valid && sl != 0)};
+        gather_records<T, PIPE, FL>(q, m, sp, rc, blk, rd, wlane);
+        // (the idle slot's texel tag becomes spec at the next evaluation: see eval_pass)
+    }
+}
+
+// The packed layout's one-round-trip gather applies (16-byte loads, every channel of the
+// slice within a lane's two rounds): the pooled speculation's precondition.
+template <typename T>
+__device__ __forceinline__ bool spec_vec1(const PC &q) {
+    constexpr int V = V16<T>::n;
+    return ((((uintptr_t)q.feat) | ((uintptr_t)q.fref)) & 15) == 0 && q.cs % V == 0 && q.ld % V == 0 &&
+           q.cb % V == 0 && (q.ce - q.cb) % V == 0 && q.ce - q.cb <= 64 * V;
+}
+
+// Wave 0's speculation (the packed layout with every channel in one round trip, i.e. the
+// headline path): wave 0 runs the LM tail between the two barriers, so it only ISSUES the
+// loads of (one pair of) its first block's predicted texels before the first barrier
+// and reduces them after the tail -- the memory round trip hides behind the barrier wait
+// and the tail instead of delaying either.  Further predicted points (rare) and further
+// blocks go through the ordinary pipeline after the tail.  Same loads and arithmetic as
+// every other gather: identical records.
+struct SpecPt {
+    int j;     // lane of the point in block 0 (-1: none)
+    int o;     // predicted texel
+    bool s;    // current slot is rec2 (the gather fills rec)
+};
+template <typename T>
+struct SpecHold {
+    GLoad<T> A;
+    SpecPt a0, a1;
+    unsigned long long rest;  // block 0's remaining wanted points
+    bool any;
+};
+
+template <typename T>
+__device__ __forceinline__ void spec0_issue(const PC &q, int mmax, SpecHold<T> &h) {
+    constexpr int V = V16<T>::n;
+    const int lane = threadIdx.x & 63, l32 = lane & 31;
+    const bool hi = lane >= 32;
+    const int *tex = lds_tex(mmax, true), *spec = lds_spec(mmax, true), *slot = lds_slot(mmax, true);
+    const int *tex2 = lds_tex2(mmax, true);
+    const bool valid = lane < q.M;
+    const int sp = valid ? spec[lane] : -1, sl = slot[lane];
+    unsigned long long m = __ballot(valid && sp >= 0 && sp != tex[lane] && sp != tex2[lane]);
+    auto take = [&]() -> SpecPt {
+        if (!m) return SpecPt{-1, 0, false};
+        const int j = __builtin_ctzll(m);
+        m &= m - 1;
+        return SpecPt{j, __builtin_amdgcn_readlane(sp, j), __builtin_amdgcn_readlane(sl, j) != 0};
+    };
+    h.a0 = take();
+    h.a1 = take();
+    h.rest = m;
+    h.any = h.a0.j >= 0;
+    if (!h.any) return;
+    const T *feat = reinterpret_cast<const T *>(q.feat);
+    const T *fref = reinterpret_cast<const T *>(q.fref);
+    const int gc = q.cb + l32 * V;
+    const bool has1 = gc < q.ce, has2 = gc + 32 * V < q.ce;
+    const int gc1 = has1 ? gc : q.cb, gc2 = has2 ? gc + 32 * V : gc1;
+    auto issue = [&](GLoad<T> &g, const SpecPt &lo, const SpecPt &hp) {  // no second point: re-read the first
+        const SpecPt &p = hi && hp.j >= 0 ? hp : lo;
+        g_issue<T>(g, feat + (size_t)p.o * 3 * q.cs, fref + (size_t)(q.p0 + p.j) * q.ld, q.cs, gc1, gc2);
+    };
+    issue(h.A, h.a0, h.a1);
+}
+
+template <typename T, bool FULL>
+__device__ __forceinline__ void spec0_finish(const PC &q, int mmax, SpecHold<T> &h, long long &ngath) {
+    constexpr int V = V16<T>::n;
+    const int lane = threadIdx.x & 63, l32 = lane & 31;
+    const bool hi = lane >= 32;
+    double *rec = lds_rec(mmax), *rec2 = lds_rec2(mmax);
+    const int rs = lds_rs(mmax);
+    const int gc = q.cb + l32 * V;
+    const bool has1 = gc < q.ce, has2 = gc + 32 * V < q.ce;
+    const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
+    const bool wlane = (lane & 3) == 0 && e6 < 6;
+    auto consume = [&](const GLoad<T> &g, const SpecPt &lo, const SpecPt &hp) {
+        double v[8];
+        g_consume<T, FULL>(g, has1, has2, v);
+        const double r = reduce8_in32(v, lane);
+        const SpecPt &p = hi ? hp : lo;
+        if (wlane && p.j >= 0) (p.s ? rec : rec2)[(size_t)e6 * rs + p.j] = r;  // the idle slot
+        ngath += hp.j >= 0 ? 2 : 1;
+    };
+    if (h.any) consume(h.A, h.a0, h.a1);
+    if (h.rest) {  // block 0's points beyond the held pair
+        const int *spec = lds_spec(mmax, true), *slot = lds_slot(mmax, true);
+        const bool valid = lane < q.M;
+        const int sp = valid ? spec[lane] : -1;
+        const size_t fo = (size_t)(wlane ? e6 : 0) * rs;
+        const RecDst rd{rec + fo, rec2 + fo, __ballot(valid && slot[lane] != 0)};
+        gather_records<T, true, false>(q, h.rest, sp, 0, 0, rd, wlane);
+        ngath += __popcll(h.rest);
     }
 }
 
@@ -977,15 +1227,16 @@ __device__ __forceinline__ void gather_f_block(unsigned long long m, int rc, boo
 // Without the ratio test each block goes straight on to its chunk partials; with it the
 // loss values are parked in the records and the wave's max |rho| is returned.
 // PIPE: double-buffered gathers (latency variant: the VGPRs for two pairs in flight).
+// SP: the variant can speculate (nearest sampling; bilinear never memoises).
 // ---------------------------------------------------------------------------
-template <typename T, bool PIPE, bool FL>
+template <typename T, bool PIPE, bool FL, bool SP>
 __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ngath) {
     LMState &st = S();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l32 = lane & 31;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool hi = lane >= 32;
     const double *X = lds_X(mmax);
     double *rec = lds_rec(mmax);
-    int *tex = lds_tex(mmax);
+    int *tex = lds_tex(mmax, q.spec);
     const int rs = lds_rs(mmax);
     const T *feat = reinterpret_cast<const T *>(q.feat);
     const T *fref = reinterpret_cast<const T *>(q.fref);
@@ -993,12 +1244,11 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
     constexpr int V = V16<T>::n;
     const bool vec = ((((uintptr_t)feat) | ((uintptr_t)fref)) & 15) == 0 && cs % V == 0 && ld % V == 0 &&
                      cb % V == 0 && (ce - cb) % V == 0;
-    // one round trip per point: every channel of the slice within the two rounds of a lane
-    const bool onetrip = vec && ce - cb <= 64 * V;
-    const int gc = cb + l32 * V;                    // this lane's first channel (one-trip path)
-    const bool has1 = gc < ce, has2 = gc + 32 * V < ce;
-    const int gc1 = has1 ? gc : cb, gc2 = has2 ? gc + 32 * V : gc1;
     const bool defer = q.use_ratio != 0;
+    const bool spec_on = SP && q.spec != 0;
+    int *tex2 = lds_tex2(mmax, true), *spec = lds_spec(mmax, true), *slot = lds_slot(mmax, true);
+    float *qp = lds_qp(mmax, true);
+    double *rec2 = lds_rec2(mmax);
     double *dst_g = q.part_g;
     if (q.G > 1) dst_g += (size_t)((ufirst((int)st.c.epoch) + 1) & 1) * q.nc_max * NV;
     // the pose evaluated: one LDS broadcast read per evaluation, kept in VGPRs (moving it to
@@ -1009,7 +1259,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
 #pragma unroll
     for (int k = 0; k < 3; ++k) te[k] = st.te[k];
     double lmax = -1.0;  // -1: nothing supported seen yet
-    for (int blk = wave; blk * 64 < M; blk += NT / 64) {
+    for (int blk = wave; blk * 64 < M; blk += nwaves()) {
         const int i = blk * 64 + lane;
         const bool valid = i < M;
         // projection (model.py:303-311) and indexing_ (model.py:88-89): floor(y*Hf/H),
@@ -1017,8 +1267,23 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         // (exact products, a correctly rounded quotient of integers floors to the integer
         // quotient), computed here with invariant-multiplier division
         double Pc[3] = {0.0, 0.0, 1.0};
-        int off = -1, rc = 0;
+        int off = -1, rc = 0, pred = -1;
         Taps tp;
+        // the point's memo state, read before the projection (it does not depend on the pose)
+        const int ii = valid ? i : 0;
+        const int old = valid ? tex[ii] : -1;
+        int t2 = -1, sl = 0;
+        float qpx = 0.0f, qpy = 0.0f;
+        if (spec_on) {
+            t2 = tex2[ii];
+            sl = slot[ii];
+            qpx = qp[ii];
+            qpy = qp[mmax + ii];
+            // the last spec pass filled the idle slot with the predicted texel when it was
+            // neither slot's (spec_pass / spec_pooled apply this same test)
+            const int sp = spec[ii];
+            if (sp >= 0 && sp != old && sp != t2) t2 = sp;
+        }
         if (valid) {
             transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
             int x, y;
@@ -1029,60 +1294,51 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
                 off = row * q.Wf + col;
                 if (FL) rc = (row << 16) | col;
                 if (q.bilinear) bilinear_taps(qx, qy, q.Hf, q.Wf, q.im_w, q.im_h, tp);
+                if (spec_on) {
+                    pred = spec_target(q, qx, qy, row, col, &qpx, &qpy);
+                    qp[i] = qpx;
+                    qp[mmax + i] = qpy;
+                }
             }
         }
         // memoised gather: a point whose texel did not change keeps its record (the six
         // channel sums depend only on the texel and the point's fixed descriptor)
-        const int old = valid ? tex[i] : -1;
         // (bilinear: the taps' weights move with the pose, every supported point is sampled)
-        const bool dirty = off >= 0 && (off != old || q.no_memo || q.bilinear);
-        if (valid) tex[i] = off;
+        bool dirty = off >= 0 && (off != old || q.no_memo || q.bilinear);
+        // with speculation a point has two record slots: a new texel that the idle slot holds
+        // (predicted and gathered by spec_pass, or the texel the point just left) is a switch,
+        // any other new texel is gathered into the idle slot and switched to
+        const unsigned long long slot_b = __ballot(sl != 0);
+        const bool moved = spec_on && dirty;
+        if (moved) dirty = off != t2;
+        if (spec_on) sl ^= moved ? 1 : 0;
+        if (valid) {
+            tex[i] = off;
+            if (spec_on) {
+                tex2[i] = moved ? old : t2;
+                if (moved) slot[i] = sl;
+                spec[i] = pred;
+            }
+        }
         unsigned long long m = __ballot(dirty);
         ngath += __popcll(m);
         dbg_stamp(q.stamps, 0);
         const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
         const bool wlane = (lane & 3) == 0 && e6 < 6;
-        double *recb = rec + (size_t)(wlane ? e6 : 0) * rs + blk * 64;  // this lane's field column
-        if constexpr (FL) {
-            if (PIPE && vec && ce - cb <= 64 * V)  // one channel round per lane
-                gather_f_pipe<T, true>(m, rc, lane, feat, fref + (size_t)(p0 + blk * 64) * ld, cs, cb, ce, ld, q.Hf,
-                                       q.Wf, q.sob_norm != 0, q.sob_rep != 0, recb, wlane);
-            else
-                gather_f_block<T>(m, rc, hi, lane, feat, fref + (size_t)(p0 + blk * 64) * ld, cs, cb, ce, ld, q.Hf,
-                                  q.Wf, vec, q.sob_norm != 0, q.sob_rep != 0, recb, wlane);
-        } else if (q.bilinear) {
+        const size_t fo = (size_t)(wlane ? e6 : 0) * rs + blk * 64;  // this lane's field column
+        const RecDst rd{rec + fo, spec_on ? rec2 + fo : rec + fo, slot_b};
+        if (!FL && q.bilinear) {
             gather_bil_block<T>(m, tp, hi, lane, feat, fref + (size_t)(p0 + blk * 64) * ld, cs, cb, ce, ld, vec,
-                                recb, wlane);
-        } else if (PIPE && onetrip) {
-            // double-buffered pairs: the next pair's loads are issued before this pair's
-            // channel sums are reduced (one exposed round trip per block, not one per pair)
-            if (ce - cb == 64 * V)
-                gather_pipe<T, true>(m, off, hi, lane, feat + 0, fref + (size_t)(p0 + blk * 64) * ld, cs, ld, gc1, gc2,
-                                     has1, has2, recb, wlane);
-            else
-                gather_pipe<T, false>(m, off, hi, lane, feat + 0, fref + (size_t)(p0 + blk * 64) * ld, cs, ld, gc1,
-                                      gc2, has1, has2, recb, wlane);
-        } else {
-            while (m) {  // wave-uniform: two dirty points per trip, one per half-wave
-                const GPair pp = pick_pair(m, off, hi);
-                const int ii = blk * 64 + pp.j;
-                const T *t = feat + (size_t)pp.to * 3 * cs;
-                const T *rf = fref + (size_t)(p0 + ii) * ld;
-                double v[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = 0.0;
-                if (vec) gather_half<T, true>(t, rf, cs, cb, ce, l32, v);
-                else gather_half<T, false>(t, rf, cs, cb, ce, l32, v);
-                const double r = reduce8_in32(v, lane);
-                if (wlane && (!hi || pp.two)) recb[pp.j] = r;
-            }
+                                rd, wlane);
+        } else if (m) {
+            gather_records<T, PIPE, FL>(q, m, off, rc, blk, rd, wlane);
         }
         // the records just written are read by other lanes of this wave: LDS operations of
         // a wave complete in order; the clobber keeps the compiler from reordering them
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         dbg_stamp(q.stamps, 1);
         const bool sup = off >= 0;
-        const double *r = rec + (valid ? i : 0);
+        const double *r = (sl ? rec2 : rec) + ii;  // the record slot in use
         double rho = 0.0, d1 = 0.0;
         if (sup) loss_eval(q.loss, q.alpha, 0.5 * r[0], rho, d1);
         if (defer) {
@@ -1106,7 +1362,7 @@ __device__ __forceinline__ void contrib_pass(const PC &q, int mmax) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const double *X = lds_X(mmax);
     const double *rec = lds_rec(mmax);
-    const int *tex = lds_tex(mmax);
+    const int *tex = lds_tex(mmax, q.spec);
     const int rs = lds_rs(mmax);
     const double limit = ufirst(st.rho_max) * st.c.ratio_thr;
     double *dst_g = q.part_g;
@@ -1116,15 +1372,17 @@ __device__ __forceinline__ void contrib_pass(const PC &q, int mmax) {
     for (int k = 0; k < 9; ++k) Re[k] = ufirst(st.Re[k]);
 #pragma unroll
     for (int k = 0; k < 3; ++k) te[k] = ufirst(st.te[k]);
-    for (int blk = wave; blk * 64 < q.M; blk += NT / 64) {
+    for (int blk = wave; blk * 64 < q.M; blk += nwaves()) {
         const int i = blk * 64 + lane;
         const bool valid = i < q.M;
         const bool sup = valid && tex[i] >= 0;
         double Pc[3] = {0.0, 0.0, 1.0};
         if (sup) transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
-        const double *r = rec + (valid ? i : 0);
+        const int ii = valid ? i : 0;
+        const double *r = rec + ii;  // rho, rho' (fields 6, 7: slot 0 only)
+        const double *rs6 = (q.spec && lds_slot(mmax, true)[ii]) ? lds_rec2(mmax) + ii : r;  // the sums' slot
         const bool kept = sup && fabs(r[6 * rs]) < limit;
-        contrib_block(q, mmax, blk, sup, kept, r[6 * rs], r[7 * rs], r, rs, Pc, dst_g);
+        contrib_block(q, mmax, blk, sup, kept, r[6 * rs], r[7 * rs], rs6, rs, Pc, dst_g);
     }
 }
 
@@ -1141,7 +1399,7 @@ __device__ __forceinline__ double combine_final_wave(int mmax, bool team) {
     const int NC = c.NC;
     double t = 0.0;
     if (!team) {
-        const double *src = lds_part(mmax);
+        const double *src = lds_part(mmax, c.spec);
         double v[4];
         for (int r0 = h; r0 < NC; r0 += 8) {  // four loads in flight, adds in chunk order
 #pragma unroll
@@ -1444,7 +1702,7 @@ __device__ __forceinline__ void lm_update_wave(double tot, bool stamps) {
 // VAR_NEAREST (any loss / mode, nearest) or VAR_BILINEAR -- constant-folding the other
 // paths out shortens the per-point code and frees registers.
 template <typename T, int WPS, bool TEAM, bool RATIO, int VAR>
-__global__ __launch_bounds__(NT, WPS) void lm_kernel(LaunchArgs a) {
+__global__ __launch_bounds__(WPS == WPS_THROUGHPUT ? NT_THROUGHPUT : NT, 2) void lm_kernel(LaunchArgs a) {
     LMState &st = S();
     const int G = a.G;
     // XCD-aware team placement: members of one team share blockIdx % gw (the same XCD
@@ -1472,7 +1730,9 @@ __global__ __launch_bounds__(NT, WPS) void lm_kernel(LaunchArgs a) {
         c.n_iters = a.opt.n_iters;
         c.use_ratio = a.opt.use_ratio;
         c.loss = a.opt.loss;
-        c.no_memo = a.opt.no_memo;
+        c.no_memo = a.opt.no_memo == 1;  // 2: memoised without speculation (a.spec = 0)
+        c.spec = a.spec;
+        c.dbg = a.dbg;
         c.sampling = a.opt.sampling;
         c.sobel_flags = a.opt.sobel_flags;
         c.stamps_on = a.stamps != nullptr;
@@ -1498,18 +1758,42 @@ __global__ __launch_bounds__(NT, WPS) void lm_kernel(LaunchArgs a) {
         long long ngath = 0;  // texel gathers of this wave for this problem
         while (!st.done) {
             // project, gather, loss (+ partials)
-            const double lmax = eval_pass<T, WPS == WPS_LATENCY, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST)>(q, mmax, ngath);
+            // (double-buffered gathers in both builds; speculation in the latency build only)
+            const double lmax = eval_pass<T, true, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST),
+                                          VAR != VAR_BILINEAR && WPS == WPS_LATENCY>(q, mmax, ngath);
             if (q.use_ratio) {
                 if (!ratio_exchange(lmax)) break;
                 contrib_pass(q, mmax);
             }
+            // speculation: every wave for its own blocks -- wave 0 issues the loads of its first
+            // block's predictions now and reduces them after the tail when the packed one-round-
+            // trip gather applies (held), else it speculates entirely before the barrier
+            constexpr bool FLV = VAR == VAR_F_GM || VAR == VAR_F_NEAREST;
+            const bool held = !FLV && WPS == WPS_LATENCY && spec_vec1<T>(q);
+            SpecHold<T> hold;
+            if (VAR != VAR_BILINEAR && WPS == WPS_LATENCY && q.spec && tid < 64) {
+                if (held) spec0_issue<T>(q, mmax, hold);
+                else spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath);
+                dbg_stamp(q.stamps, 12);  // wave 0's own speculation (before the barrier)
+            }
             if (TEAM) team_arrive();
             else __syncthreads();
-            if (tid < 64 && (!TEAM || team_wait())) {
-                dbg_stamp(q.stamps, 3);  // slowest wave + exchange
-                const double tot = combine_final_wave(mmax, TEAM);
-                dbg_stamp(q.stamps, 4);
-                lm_update_wave(tot, q.stamps);
+            if (tid < 64) {
+                if (!TEAM || team_wait()) {
+                    dbg_stamp(q.stamps, 3);  // slowest wave + exchange
+                    const double tot = combine_final_wave(mmax, TEAM);
+                    dbg_stamp(q.stamps, 4);
+                    lm_update_wave(tot, q.stamps);
+                }
+                if (VAR != VAR_BILINEAR && WPS == WPS_LATENCY && q.spec && held) {
+                    if (q.ce - q.cb == 64 * V16<T>::n) spec0_finish<T, true>(q, mmax, hold, ngath);
+                    else spec0_finish<T, false>(q, mmax, hold, ngath);
+                    spec_pass<T, true, false>(q, mmax, ngath, nwaves());  // wave 0's further blocks
+                }
+            } else if (VAR != VAR_BILINEAR && WPS == WPS_LATENCY && q.spec) {
+                // the other waves gather their blocks' predicted next texels meanwhile
+                spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath);
+                dbg_stamp(q.stamps, 4);  // waves >= 1: the speculative gathers
             }
             __syncthreads();
             dbg_stamp(q.stamps, 7);  // pose update + barrier

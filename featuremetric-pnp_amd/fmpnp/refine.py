@@ -255,10 +255,13 @@ def bind_layout(problems, options):
 
 def make_options(n_iters, lambda0=0.01, loss=_lib.SQUARED, barron_alpha=0.0, ratio_threshold=None,
                  dtype=_lib.F32, mode=_lib.MODE_FORWARD, wgs_per_problem=0, max_teams=0, memoize=True,
-                 sampling="nearest"):
+                 sampling="nearest", speculate=True):
     """fmpnp_options.  sampling: "nearest" (the reference's indexing_, model.py:74-97) or
     "bilinear" (extension: 2x2 taps of f, gx, gy; definition in fmpnp_device.h bilinear_taps,
-    checked against the oracle's restatement -- no reference counterpart, parity unpinned)."""
+    checked against the oracle's restatement -- no reference counterpart, parity unpinned).
+    memoize: re-gather a point's texel only when it changed; speculate (memoised nearest
+    forward runs): gather the predicted next texels beside the LM tail.  Neither changes
+    the results."""
     o = _lib.Options()
     o.mode = int(mode)
     o.n_iters = int(n_iters)
@@ -271,7 +274,7 @@ def make_options(n_iters, lambda0=0.01, loss=_lib.SQUARED, barron_alpha=0.0, rat
     o.dtype = int(dtype)
     o.wgs_per_problem = int(wgs_per_problem)
     o.max_teams = int(max_teams)
-    o.no_memo = 0 if memoize else 1
+    o.no_memo = (0 if speculate else 2) if memoize else 1
     return o
 
 

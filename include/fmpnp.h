@@ -99,7 +99,9 @@ typedef struct {
     int max_teams;          /* cap on concurrently resident problem teams; 0 = auto */
     int no_memo;            /* 1: re-gather every point's texel at every evaluation (the
                                reference's data movement); 0 (default): re-gather only points
-                               whose texel changed -- bit-identical results */
+                               whose texel changed, and gather the texels that points are
+                               predicted to move to next beside the LM tail (speculation);
+                               2: memoised without speculation -- all bit-identical results */
     int layout;             /* fmpnp_layout of every problem's feat */
     int sobel_flags;        /* FMPNP_LAYOUT_F: bit 0 normalized (/8), bit 1 replicate padding
                                (the flags fmpnp_pack_features would have been given) */

@@ -126,3 +126,27 @@ def test_cfg2_layout_f_50_iters():
     prob = packed_problem(inp, "f")
     (res,), (tr,) = rf.refine([prob], rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32), trace=True)
     check(res, tr, ores, otr, "layout f")
+
+
+@pytest.mark.parametrize("layout,init,ratio,wgs", [("fgrad", "easy", None, 0), ("fgrad", "hard", 0.8, 0),
+                                                   ("f", "hard", None, 0), ("fgrad", "hard", None, 3)])
+def test_speculative_gathers_change_nothing(layout, init, ratio, wgs):
+    """The speculative next-texel gathers (fmpnp_lm_impl.h spec_pass) only move where a
+    record's sums come from: poses, costs, support counts and the LM schedule are
+    bit-identical with speculation on, off, and with memoisation off."""
+    inp = synth.problem_inputs(512, 256, 240, 320, seed=21, device=DEV, init=init)
+    prob = packed_problem(inp, layout)
+    runs = []
+    for memo, spec in ((True, True), (True, False), (False, False)):
+        o = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, ratio_threshold=ratio, dtype=_lib.F32,
+                            wgs_per_problem=wgs, memoize=memo, speculate=spec)
+        (res,), (tr,) = rf.refine([prob], o, trace=True)
+        runs.append((res, tr))
+    (a, ta), (b, tb), (c, tc) = runs
+    for r, t in ((b, tb), (c, tc)):
+        assert np.array_equal(a["R"], r["R"]) and np.array_equal(a["t"], r["t"])
+        assert a["best_cost"] == r["best_cost"] and a["n_evals"] == r["n_evals"]
+        np.testing.assert_array_equal(ta["cost"], t["cost"])
+        np.testing.assert_array_equal(ta["n_supported"], t["n_supported"])
+    # speculation reads more texels in total, but the evaluations themselves gather fewer
+    assert c["texel_gathers"] >= b["texel_gathers"]
