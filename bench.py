@@ -65,6 +65,7 @@ def parse():
     ap.add_argument("--init", choices=["easy", "hard"], default="easy")
     ap.add_argument("--ratio", type=float, default=None, help="ratio-test threshold (model.py:324-336)")
     ap.add_argument("--no-memo", action="store_true", help="re-gather every texel at every evaluation")
+    ap.add_argument("--no-spec", action="store_true", help="memoised without the speculative next-texel gathers")
     ap.add_argument("--sampling", choices=["nearest", "bilinear"], default="nearest")
     ap.add_argument("--layout", choices=["fgrad", "f"], default="fgrad")
     ap.add_argument("--wgs", type=int, default=0, help="workgroups per query (0 = planner)")
@@ -82,7 +83,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def workload_tag(B, init, ratio, memo, sampling, layout):
+def workload_tag(B, init, ratio, memo, sampling, layout, spec=True):
     """Key of a workload in profiles/r02_pmc_<tag>.json."""
     t = f"b{B}_{init}"
     if ratio is not None:
@@ -93,6 +94,8 @@ def workload_tag(B, init, ratio, memo, sampling, layout):
         t += "_" + sampling
     if layout != "fgrad":
         t += "_layout" + layout
+    if memo and not spec:
+        t += "_nospec"
     return t
 
 
@@ -180,7 +183,8 @@ def main():
         log(f"[bench] setup {B} queries/GPU in {time.time() - t0:.1f}s "
             f"({torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB resident)")
     opts = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, ratio_threshold=args.ratio, dtype=_lib.F32,
-                           wgs_per_problem=args.wgs, memoize=memo, sampling=args.sampling)
+                           wgs_per_problem=args.wgs, memoize=memo, sampling=args.sampling,
+                           speculate=not args.no_spec)
     batch = rf.AsyncBatch(probs, opts)
 
     # ---------------- warmup ----------------
@@ -205,7 +209,7 @@ def main():
     if any(s & _lib.STATUS_SYNC_TIMEOUT for s in statuses):
         raise RuntimeError("sync timeout in the LM kernel")
     value = B * world * args.steps / elapsed
-    tag = workload_tag(B, args.init, args.ratio, memo, args.sampling, args.layout)
+    tag = workload_tag(B, args.init, args.ratio, memo, args.sampling, args.layout, not args.no_spec)
 
     extras = {}
     if rank == 0 and args.legs:
@@ -232,6 +236,7 @@ def main():
                        "points": N_PTS, "channels": C, "feature_map": f"{HF}x{WF}", "image": f"{4 * HF}x{4 * WF}",
                        "iters": ITERS, "loss": "geman_mcclure", "lambda0": 0.01, "texel_storage": "f32",
                        "init": args.init, "ratio_threshold": args.ratio, "memoised": memo,
+                       "speculative_gathers": memo and not args.no_spec,
                        "sampling": args.sampling, "layout": args.layout,
                        "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"query sharding x{world} (no collectives)", "launch": launch},
@@ -312,8 +317,8 @@ def run_legs(args, dev, probs, feats, inputs, opts, res_main, rf, _lib, synth):
         out["ratio08"]["kernel_variant"] = "RATIO=true"
     if "no_spec" in args.legs and memo:  # memoised, without the speculative next-texel gathers
         ms, r = time_launches(rf.AsyncBatch(probs, opt(speculate=False)), 10, stream)
-        out["no_spec"] = leg_summary(workload_tag(B, args.init, args.ratio, memo, args.sampling, args.layout) +
-                                     "_nospec", ms, r, B, args.sampling, args.layout, base=res_main)
+        out["no_spec"] = leg_summary(workload_tag(B, args.init, args.ratio, memo, args.sampling, args.layout, False),
+                                     ms, r, B, args.sampling, args.layout, base=res_main)
     if "no_memo" in args.legs and memo:  # the reference's data movement: every texel re-read
         ms, r = time_launches(rf.AsyncBatch(probs, opt(memoize=False)), 5, stream)
         out["no_memo"] = leg_summary(workload_tag(B, args.init, args.ratio, False, args.sampling, args.layout), ms,

@@ -11,11 +11,14 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 # tag|bench flags
 WORKLOADS="${WORKLOADS:-b128_easy|
+b128_easy_nospec|--no-spec
 b128_hard|--init hard
+b128_hard_ratio0.8|--init hard --ratio 0.8
 b128_easy_ratio0.8|--ratio 0.8
 b128_easy_nomemo|--no-memo
 b128_easy_bilinear|--sampling bilinear
-b128_easy_layoutf|--layout f}"
+b128_easy_layoutf|--layout f
+b1024_easy|}"
 BASE="--legs none --steps 5 --warmup 1"
 while IFS='|' read -r tag flags; do
   [ -z "$tag" ] && continue
@@ -26,6 +29,9 @@ while IFS='|' read -r tag flags; do
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$D/pmc_fetch" -o run -- python3 "$REPO/bench.py" $BASE --batch $B $flags > /dev/null 2> "$D/pmc_fetch.err" || { echo "fetch $tag failed"; tail -20 "$D/pmc_fetch.err"; exit 1; }
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$D/pmc_write" -o run -- python3 "$REPO/bench.py" $BASE --batch $B $flags > /dev/null 2> "$D/pmc_write.err" || { echo "write $tag failed"; tail -20 "$D/pmc_write.err"; exit 1; }
   python3 "$REPO/tools/pmc_summary.py" "$D" "$B" "$D/summary.json" auto "$tag" || exit 1
+  # keep what is committed (summary + kernel stats); the per-dispatch CSVs stay on the box
+  find "$D/trace" -name "*kernel_stats.csv" -exec cp {} "$D/kernel_stats.csv" \;
+  rm -rf "$D/trace" "$D/pmc_fetch" "$D/pmc_write"
 done <<< "$WORKLOADS"
 if [ -n "$SQ" ]; then
   D="$OUT/sq"; mkdir -p "$D"; i=0
@@ -45,5 +51,6 @@ for k in sorted(tot):
     print(f"{k:28s} {tot[k] / max(1, len(n[k])):16.0f}  (per dispatch, {len(n[k])} dispatches)")
 PY
   cat "$D/summary.txt"
+  rm -rf "$D"/p1 "$D"/p2
 fi
 for f in "$OUT"/*/summary.json; do python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['tag'], d['kernel'], d['kernel_avg_ns'], d['hbm_bytes_per_launch'])" "$f"; done
