@@ -89,8 +89,8 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     // speculative next-texel gathers (fmpnp_lm_impl.h spec_pass): memoised nearest sampling of
     // a forward run; no_memo = 2 keeps the memo without them (a measurement knob)
     // (the f-only layout's nine-texel gathers are too heavy to hide: B=128 0.68 -> 0.75 ms with it)
-    P.spec = (opt->no_memo == 0 && opt->sampling == FMPNP_NEAREST && opt->mode == FMPNP_MODE_FORWARD &&
-              opt->layout == FMPNP_LAYOUT_FGRAD) ? 1 : 0;
+    P.spec = (FMPNP_SPEC && opt->no_memo == 0 && opt->sampling == FMPNP_NEAREST &&
+              opt->mode == FMPNP_MODE_FORWARD && opt->layout == FMPNP_LAYOUT_FGRAD) ? 1 : 0;
     auto lds_for = [&](int G) {
         const int m = ((P.nc_max + G - 1) / G) * CH;
         return lds_fixed_bytes() + (int)lm_dyn_lds_bytes(m, P.nc_max, P.spec != 0);

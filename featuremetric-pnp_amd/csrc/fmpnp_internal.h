@@ -5,6 +5,14 @@
 
 #include "fmpnp.h"
 
+// Speculative next-texel gathers (fmpnp_lm_impl.h spec_pass): measured, not adopted -- the
+// gathers they take off the evaluation are paid back by the extra per-point work and register
+// pressure (B=128: 0.367 ms with them, 0.365 ms compiled out).  Build with
+// -DFMPNP_SPEC=1 to measure them.
+#ifndef FMPNP_SPEC
+#define FMPNP_SPEC 0
+#endif
+
 namespace fmpnp {
 
 constexpr int NT = 512;         // threads per workgroup of the LM kernel (8 waves)

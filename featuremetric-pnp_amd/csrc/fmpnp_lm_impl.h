@@ -48,6 +48,8 @@
 
 namespace fmpnp {
 
+constexpr bool kSpecBuild = FMPNP_SPEC != 0;
+
 // dynamic LDS of the LM kernel (the only kernel in this file that uses LDS)
 extern __shared__ __attribute__((aligned(16))) unsigned char lm_lds[];
 
@@ -1760,7 +1762,7 @@ __global__ __launch_bounds__(WPS == WPS_THROUGHPUT ? NT_THROUGHPUT : NT, 2) void
             // project, gather, loss (+ partials)
             // (double-buffered gathers in both builds; speculation in the latency build only)
             const double lmax = eval_pass<T, true, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST),
-                                          VAR != VAR_BILINEAR && WPS == WPS_LATENCY>(q, mmax, ngath);
+                                          kSpecBuild && VAR != VAR_BILINEAR && WPS == WPS_LATENCY>(q, mmax, ngath);
             if (q.use_ratio) {
                 if (!ratio_exchange(lmax)) break;
                 contrib_pass(q, mmax);
@@ -1771,7 +1773,7 @@ __global__ __launch_bounds__(WPS == WPS_THROUGHPUT ? NT_THROUGHPUT : NT, 2) void
             constexpr bool FLV = VAR == VAR_F_GM || VAR == VAR_F_NEAREST;
             const bool held = !FLV && WPS == WPS_LATENCY && spec_vec1<T>(q);
             SpecHold<T> hold;
-            if (VAR != VAR_BILINEAR && WPS == WPS_LATENCY && q.spec && tid < 64) {
+            if (kSpecBuild && VAR != VAR_BILINEAR && WPS == WPS_LATENCY && q.spec && tid < 64) {
                 if (held) spec0_issue<T>(q, mmax, hold);
                 else spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath);
                 dbg_stamp(q.stamps, 12);  // wave 0's own speculation (before the barrier)
@@ -1785,12 +1787,12 @@ __global__ __launch_bounds__(WPS == WPS_THROUGHPUT ? NT_THROUGHPUT : NT, 2) void
                     dbg_stamp(q.stamps, 4);
                     lm_update_wave(tot, q.stamps);
                 }
-                if (VAR != VAR_BILINEAR && WPS == WPS_LATENCY && q.spec && held) {
+                if (kSpecBuild && VAR != VAR_BILINEAR && WPS == WPS_LATENCY && q.spec && held) {
                     if (q.ce - q.cb == 64 * V16<T>::n) spec0_finish<T, true>(q, mmax, hold, ngath);
                     else spec0_finish<T, false>(q, mmax, hold, ngath);
                     spec_pass<T, true, false>(q, mmax, ngath, nwaves());  // wave 0's further blocks
                 }
-            } else if (VAR != VAR_BILINEAR && WPS == WPS_LATENCY && q.spec) {
+            } else if (kSpecBuild && VAR != VAR_BILINEAR && WPS == WPS_LATENCY && q.spec) {
                 // the other waves gather their blocks' predicted next texels meanwhile
                 spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath);
                 dbg_stamp(q.stamps, 4);  // waves >= 1: the speculative gathers

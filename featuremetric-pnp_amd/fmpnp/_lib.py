@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (load torch's HIP runtime before libfmpnp)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libfmpnp.so")
+LIB_PATH = os.environ.get("FMPNP_LIB_PATH") or os.path.join(HERE, "lib", "libfmpnp.so")  # override: A/B builds
 
 # enums / constants (include/fmpnp.h)
 SQUARED, HUBER, CAUCHY, GEMAN_MCCLURE, BARRON = 0, 1, 2, 3, 4
