@@ -18,6 +18,15 @@ int main() {
         const double e = fmax(es, ec) / 2.220446049250313e-16;  // in units of eps (|sin|, |cos| <= 1)
         if (e > worst) { worst = e; worst_x = x; }
     }
+    // larger steps, log-spaced: the two-part Cody-Waite reduction up to 2^19 pi/2, the
+    // out-of-line library routine beyond (a near-singular step; the reference's torch.sin/cos)
+    for (int i = 0; i <= 200000; ++i) {
+        const double x = 200.0 * pow(1e10, i / 200000.0);  // 200 .. 2e12 rad
+        double s, c;
+        fmpnp::sincos_rr(x, s, c);
+        const double e = fmax(fabs(s - sin(x)), fabs(c - cos(x))) / 2.220446049250313e-16;
+        if (e > worst) { worst = e; worst_x = x; }
+    }
     double s, c;
     fmpnp::sincos_rr(INFINITY, s, c);
     const bool nan_ok = isnan(s) && isnan(c);

@@ -170,3 +170,37 @@ def test_pipeline_raises_index_error_for_out_of_map_inliers():
                           model_kwargs=dict(n_iters=3, loss_fn=fmpnp.geman_mcclure_loss))
     with pytest.raises(IndexError):
         pipe.run([[(q, r, pred, z["in_K"])], [(q, r, bad, z["in_K"])]])
+
+
+@pytest.mark.gpu
+def test_pipeline_waits_for_maps_produced_on_the_callers_stream():
+    """The hypercolumns are written on the caller's (current) stream by a slow chain of
+    kernels immediately before run(): the pipeline's prep stream must wait for them (a
+    network's output is produced exactly like this).  Every batch's poses equal the
+    reference's feature_pnp outputs."""
+    import torch
+    import fmpnp
+    from fmpnp.pipeline import RefinePipeline
+    z, entries = golden_entries(n_ok=1, n_fail=0)
+    meta = json.loads(str(z["meta"]))
+    dev = torch.device("cuda", 0)
+    q_src = torch.from_numpy(z["in_query"]).to(dev).double()
+    r_src = torch.from_numpy(z["in_ref"]).to(dev).double()
+    pred = rp.prediction_from_entry(next(iter(entries.values())))
+    pipe = RefinePipeline(tuple(meta["image_shape"]), storage=torch.float64, depth=2,
+                          model_kwargs=dict(n_iters=meta["n_iters"], loss_fn=fmpnp.geman_mcclure_loss,
+                                            lambda_=meta["lambda0"], ratio_threshold=None))
+    for _ in range(3):
+        q = torch.full_like(q_src, float("nan"))
+        r = torch.full_like(r_src, float("nan"))
+        torch.cuda.synchronize()
+        # ~tens of ms of work on the current stream, then the real maps land in q and r
+        x = torch.randn((2048, 2048), device=dev)
+        for _ in range(40):
+            x = torch.tanh(x @ x * 1e-3)
+        q.copy_(q_src + 0.0 * x[0, 0].double())
+        r.copy_(r_src + 0.0 * x[0, 1].double())
+        out = pipe.run([[(q, r, pred, z["in_K"])] * 2])
+        for res in out[0]:
+            np.testing.assert_allclose(res["R"], z["out_R"], atol=1e-9)
+            np.testing.assert_allclose(res["t"], z["out_t"], atol=1e-9)
