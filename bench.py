@@ -57,7 +57,7 @@ LEGS = ["single", "hard", "ratio", "no_spec", "no_memo", "bilinear", "layout_f",
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--steps", type=int, default=8000)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=128, help="queries per GPU (weak scaling)")
     ap.add_argument("--global-batch", type=int, default=0,
@@ -116,7 +116,7 @@ def gather_bytes_rule(sampling, layout):
     if layout == "f":
         return 40 * C, "9 neighbour texels x 4C (f) + 4C fref per gather"
     if sampling == "bilinear":
-        return 52 * C, "4 taps x (f, gx, gy) 4C + 4C fref per sampled point"
+        return 52 * C, "4 taps x (f, gx, gy) 4C + 4C fref per sampled cell"
     return 16 * C, "(f, gx, gy, fref) x 4C per gather"
 
 
@@ -236,7 +236,7 @@ def main():
                        "points": N_PTS, "channels": C, "feature_map": f"{HF}x{WF}", "image": f"{4 * HF}x{4 * WF}",
                        "iters": ITERS, "loss": "geman_mcclure", "lambda0": 0.01, "texel_storage": "f32",
                        "init": args.init, "ratio_threshold": args.ratio, "memoised": memo,
-                       "speculative_gathers": memo and not args.no_spec,
+                       "speculative_gathers": memo and not args.no_spec and _lib.spec_build(),
                        "sampling": args.sampling, "layout": args.layout,
                        "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"query sharding x{world} (no collectives)", "launch": launch},
@@ -315,7 +315,7 @@ def run_legs(args, dev, probs, feats, inputs, opts, res_main, rf, _lib, synth):
         out["ratio08"] = leg_summary(workload_tag(B, args.init, 0.8, memo, args.sampling, args.layout), ms, r, B,
                                      args.sampling, args.layout)
         out["ratio08"]["kernel_variant"] = "RATIO=true"
-    if "no_spec" in args.legs and memo:  # memoised, without the speculative next-texel gathers
+    if "no_spec" in args.legs and memo and _lib.spec_build():  # memoised, without the speculative gathers
         ms, r = time_launches(rf.AsyncBatch(probs, opt(speculate=False)), 10, stream)
         out["no_spec"] = leg_summary(workload_tag(B, args.init, args.ratio, memo, args.sampling, args.layout, False),
                                      ms, r, B, args.sampling, args.layout, base=res_main)
@@ -324,9 +324,16 @@ def run_legs(args, dev, probs, feats, inputs, opts, res_main, rf, _lib, synth):
         out["no_memo"] = leg_summary(workload_tag(B, args.init, args.ratio, False, args.sampling, args.layout), ms,
                                      r, B, args.sampling, args.layout, base=res_main)
     if "bilinear" in args.legs and args.sampling == "nearest" and args.layout == "fgrad":  # extension
-        ms, r = time_launches(rf.AsyncBatch(probs, opt(sampling="bilinear")), 3, stream)
+        # the cell memo (default), and every supported point sampled at every evaluation
+        ms, r = time_launches(rf.AsyncBatch(probs, opt(sampling="bilinear")), 10, stream)
         out["bilinear"] = leg_summary(workload_tag(B, args.init, args.ratio, memo, "bilinear", "fgrad"), ms, r, B,
                                       "bilinear", "fgrad")
+        out["bilinear"]["launch"] = _lib.last_launch()
+        ms, r2 = time_launches(rf.AsyncBatch(probs, opt(sampling="bilinear", memoize=False)), 3, stream)
+        out["bilinear_direct"] = leg_summary(workload_tag(B, args.init, args.ratio, False, "bilinear", "fgrad"), ms,
+                                             r2, B, "bilinear", "fgrad")
+        out["bilinear_direct"]["max_rot_diff_vs_memo_rad"] = float(max(rot_angle(a["R"], b["R"])
+                                                                       for a, b in zip(r, r2)))
     if "layout_f" in args.legs and args.layout == "fgrad" and args.sampling == "nearest":
         fp = []
         for q, inp in enumerate(inputs):

@@ -35,11 +35,13 @@ int elem_size(int dtype) { return dtype == FMPNP_F64 ? 8 : 4; }
 
 // Per-problem bounds shared by the LM launch and fmpnp_point_costs: every projected pixel
 // maps to a texel < Hf*Wf through 32-bit unsigned products, and the map size is bounded.
-int validate_problem(const fmpnp_problem &p, int layout) {
+int validate_problem(const fmpnp_problem &p, int layout, int sampling) {
     if (p.N < 0 || p.Hf <= 0 || p.Wf <= 0 || p.im_width <= 0 || p.im_height <= 0) return FMPNP_EINVAL;
     if (p.c_begin < 0 || p.c_end < p.c_begin || p.c_end > p.cstride || p.c_end > p.ld_ref) return FMPNP_EINVAL;
     if (p.N > 0 && (!p.feat || !p.fref || !p.pts3d)) return FMPNP_EINVAL;
     if (layout == FMPNP_LAYOUT_F && (p.Hf >= 65536 || p.Wf >= 65536)) return FMPNP_ETOOBIG;
+    // bilinear cell keys pack (row + 1, column + 1) into 15 + 16 bits
+    if (sampling == FMPNP_BILINEAR && (p.Hf >= 32768 || p.Wf >= 65535)) return FMPNP_ETOOBIG;
     // the packed map must hold 3*cstride per texel
     if ((long long)p.Hf * p.Wf * 3 * (long long)p.cstride > (1LL << 40)) return FMPNP_ETOOBIG;
     // pixel -> texel rescale in 32-bit unsigned arithmetic: y * Hf < 2^32, x * Wf < 2^32
@@ -61,7 +63,7 @@ int validate(const fmpnp_problem *probs, int n, const fmpnp_options *opt) {
     if (opt->sobel_flags & ~3) return FMPNP_EINVAL;
     if (opt->no_memo < 0 || opt->no_memo > 2) return FMPNP_EINVAL;
     for (int i = 0; i < n; ++i) {
-        const int rc = validate_problem(probs[i], opt->layout);
+        const int rc = validate_problem(probs[i], opt->layout, opt->sampling);
         if (rc) return rc;
     }
     return 0;
@@ -91,10 +93,14 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     // (the f-only layout's nine-texel gathers are too heavy to hide: B=128 0.68 -> 0.75 ms with it)
     P.spec = (FMPNP_SPEC && opt->no_memo == 0 && opt->sampling == FMPNP_NEAREST &&
               opt->mode == FMPNP_MODE_FORWARD && opt->layout == FMPNP_LAYOUT_FGRAD) ? 1 : 0;
+    // bilinear sampling keeps each point's cell memo in LDS (at most BIL_MAX_M points per
+    // workgroup) unless no_memo asks for every point sampled every evaluation
+    const bool bil_memo = opt->sampling == FMPNP_BILINEAR && opt->no_memo != 1;
+    auto m_for = [&](int G) { return ((P.nc_max + G - 1) / G) * CH; };
     auto lds_for = [&](int G) {
-        const int m = ((P.nc_max + G - 1) / G) * CH;
-        return lds_fixed_bytes() + (int)lm_dyn_lds_bytes(m, P.nc_max, P.spec != 0);
+        return lds_fixed_bytes() + (int)lm_dyn_lds_bytes(m_for(G), P.nc_max, P.spec != 0, bil_memo);
     };
+    auto fits = [&](int G) { return lds_for(G) <= lds_cu && (!bil_memo || m_for(G) <= BIL_MAX_M); };
     // resident workgroups per CU (VGPR and LDS limits).  Hardware admission of 256-thread
     // blocks is also bounded by SGPRs: floor(800 / (ceil(sgpr/16)*16 + 16)) >= 6 for any
     // kernel (<= 112 SGPRs incl. VCC), and the API over-reports only above that
@@ -104,7 +110,7 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb,
                                                          lm_kernel_ptr(opt->dtype, P.wps, P.G > 1,
                                                                        opt->use_ratio != 0, lm_variant(*opt)),
-                                                         P.wps == WPS_THROUGHPUT ? NT_THROUGHPUT : NT, lds) !=
+                                                         P.wps == WPS_LATENCY ? NT : NT_THROUGHPUT, lds) !=
             hipSuccess)
             return 1;
         return std::max(1, std::min(nb, 6));
@@ -118,9 +124,9 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     if (opt->wgs_per_problem > 0) {
         G = std::min(opt->wgs_per_problem, P.nc_max);
     } else {
-        // (no_memo and bilinear sampling re-read every texel each evaluation: bandwidth-bound,
-        // so every CU gets a workgroup; bilinear B=128: G=2 7.32 ms vs G=1 7.75 ms)
-        const bool streaming = opt->no_memo == 1 || opt->sampling == FMPNP_BILINEAR;
+        // (no_memo re-reads every texel each evaluation: bandwidth-bound, so every CU gets a
+        // workgroup; bilinear without the memo at B=128: G=2 7.32 ms vs G=1 7.75 ms)
+        const bool streaming = opt->no_memo == 1;
         G = (n <= 0 || (2L * n >= ncu && !streaming)) ? 1 : (ncu + n - 1) / n;
         // memoised packed-gradient loop on problems of <= 512 points: the evaluation is a
         // latency chain and a member's exchange costs about what the split saves, so one
@@ -128,12 +134,13 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
         // spread-out G=8: B=8 0.307 vs 0.326, B=16 0.311 vs 0.328, B=32 0.315 vs 0.332,
         // B=1 0.305 vs 0.313).  Larger problems keep spreading (cfg5, 2048 points at
         // C=512: G=4 0.64 ms vs G=32 0.58 ms at B=1)
-        if (!streaming && opt->layout == FMPNP_LAYOUT_FGRAD && P.nc_max <= 8) G = 1;
+        // (not bilinear: its memo builds are VALU work that more CUs share)
+        if (!streaming && !bil_memo && opt->layout == FMPNP_LAYOUT_FGRAD && P.nc_max <= 8) G = 1;
         G = std::max(1, std::min(G, P.nc_max));
     }
     G = std::min(G, MAX_G);
-    while (G < std::min(P.nc_max, MAX_G) && lds_for(G) > lds_cu) ++G;
-    if (lds_for(G) > lds_cu) return FMPNP_ETOOBIG;
+    while (G < std::min(P.nc_max, MAX_G) && !fits(G)) ++G;
+    if (!fits(G)) return FMPNP_ETOOBIG;
     P.G = G;
     P.mmax = ((P.nc_max + G - 1) / G) * CH;
     P.lds = lds_for(G);
@@ -143,10 +150,11 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     // CU busy there is no idle memory time to hide it in).  FMPNP_LM_WPS=2|4 forces a build.
     const char *wps_env = getenv("FMPNP_LM_WPS");
     const int want = wps_env ? atoi(wps_env) : 0;
-    const bool tp_ok = opt->layout == FMPNP_LAYOUT_FGRAD && G == 1 && (long)n >= ncu &&
-                       2 * (lds_fixed_bytes() + (int)lm_dyn_lds_bytes(P.mmax, P.nc_max, false)) <= lds_cu;
+    const bool tp_ok = !bil_memo && opt->layout == FMPNP_LAYOUT_FGRAD && G == 1 && (long)n >= ncu &&
+                       2 * (lds_fixed_bytes() + (int)lm_dyn_lds_bytes(P.mmax, P.nc_max, false, bil_memo)) <= lds_cu;
     const bool tp = tp_ok && (want == WPS_THROUGHPUT || (want == 0 && (long)n >= 2L * ncu));
     P.wps = tp ? WPS_THROUGHPUT : WPS_LATENCY;
+    if (bil_memo) P.wps = WPS_WIDE;  // the memo build's registers: one wave per SIMD
     if (tp) {
         P.spec = 0;
         P.lds = lds_for(G);
@@ -189,9 +197,11 @@ extern "C" {
 
 int fmpnp_abi_version(void) { return FMPNP_ABI_VERSION; }
 
+#define FMPNP_STR2(x) #x
+#define FMPNP_STR(x) FMPNP_STR2(x)
 const char *fmpnp_build_info(void) {
-    return "fmpnp gfx950: lm_kernel(NT=512 wave-owned blocks, CH=64, NV=32, fp64 accumulation), pack_kernel(Sobel+HWC3), "
-           "gather_ref_kernel";
+    return "fmpnp gfx950: lm_kernel(NT=512 wave-owned blocks, CH=64, NV=32, fp64 accumulation, bilinear cell memo), "
+           "pack_kernel(Sobel+HWC3), gather_ref_kernel; speculative_gathers=" FMPNP_STR(FMPNP_SPEC);
 }
 
 int fmpnp_device_check(int device) {
@@ -255,7 +265,7 @@ int fmpnp_point_costs(const fmpnp_problem *prob, int layout, int dtype, double *
     if (p.N == 0) return 0;
     if (layout != FMPNP_LAYOUT_FGRAD && layout != FMPNP_LAYOUT_F) return FMPNP_EINVAL;
     if (p.c_end <= p.c_begin) return FMPNP_EINVAL;
-    const int rc = validate_problem(p, layout);  // the LM path's bounds (32-bit texel rescale)
+    const int rc = validate_problem(p, layout, FMPNP_NEAREST);  // the LM path's bounds (32-bit texel rescale)
     if (rc) return rc;
     if (dtype != FMPNP_F32 && dtype != FMPNP_F64) return FMPNP_EINVAL;
     if (layout == FMPNP_LAYOUT_F && dtype != FMPNP_F32) return FMPNP_EINVAL;

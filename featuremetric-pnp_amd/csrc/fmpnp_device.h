@@ -194,6 +194,8 @@ __device__ __forceinline__ bool project_px(const double *K, const double P[3], i
 struct Taps {
     int off[4];       // texel offsets (row * Wf + col): [y0x0, y0x1, y1x0, y1x1]
     double w[4];
+    double ax, ay;    // the point's position inside its cell
+    int key;          // the cell: ((y0 + 1) << 16) | (x0 + 1) of the unclamped floors (bil_cell_taps)
 };
 __device__ __forceinline__ void bilinear_taps(double qx, double qy, int Hf, int Wf, int W, int H, Taps &t) {
 #pragma clang fp contract(off)
@@ -202,6 +204,11 @@ __device__ __forceinline__ void bilinear_taps(double qx, double qy, int Hf, int 
     const double fx0 = floor(sx), fy0 = floor(sy);
     const double ax = sx - fx0, ay = sy - fy0;
     int x0 = (int)fx0, y0 = (int)fy0, x1 = x0 + 1, y1 = y0 + 1;
+    // a supported pixel has -1 <= floor <= size - 1; clamping the key's floors into that range
+    // changes no tap (every tap is clamped to the map below)
+    t.key = ((min(max(y0, -1), Hf - 1) + 1) << 16) | (min(max(x0, -1), Wf - 1) + 1);
+    t.ax = ax;
+    t.ay = ay;
     x0 = min(max(x0, 0), Wf - 1);
     x1 = min(max(x1, 0), Wf - 1);
     y0 = min(max(y0, 0), Hf - 1);
@@ -214,6 +221,15 @@ __device__ __forceinline__ void bilinear_taps(double qx, double qy, int Hf, int 
     t.w[1] = ax * (1.0 - ay);
     t.w[2] = (1.0 - ax) * ay;
     t.w[3] = ax * ay;
+}
+// The four tap offsets of a cell key (bilinear_taps' clamping, the same offsets).
+__device__ __forceinline__ void bil_cell_taps(int key, int Hf, int Wf, int o[4]) {
+    const int fy = (key >> 16) - 1, fx = (key & 0xffff) - 1;
+    const int x0 = max(fx, 0), x1 = min(fx + 1, Wf - 1), y0 = max(fy, 0), y1 = min(fy + 1, Hf - 1);
+    o[0] = y0 * Wf + x0;
+    o[1] = y0 * Wf + x1;
+    o[2] = y1 * Wf + x0;
+    o[3] = y1 * Wf + x1;
 }
 // one sampled value: fma(w11, v11, fma(w10, v10, fma(w01, v01, w00 v00)))
 __device__ __forceinline__ double sample4(const double w[4], double v0, double v1, double v2, double v3) {

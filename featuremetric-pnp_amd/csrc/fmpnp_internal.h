@@ -27,6 +27,9 @@ constexpr int MAX_G = 64;       // workgroups per problem
 // (batches of >= 2 problems per CU).  Both keep 2 waves per SIMD: up to 256 VGPRs.
 constexpr int WPS_LATENCY = 2, WPS_THROUGHPUT = 4;
 constexpr int NT_THROUGHPUT = 256;
+// WPS_WIDE = 256-thread workgroups, one wave per SIMD: up to 512 registers per lane (VGPRs +
+// AGPRs), for the bilinear cell memo (its LDS allows one workgroup per CU anyway)
+constexpr int WPS_WIDE = 1;
 
 // Kernel arguments (by value).
 struct LaunchArgs {
@@ -57,14 +60,20 @@ __host__ __device__ constexpr int lds_rs(int mmax) { return mmax + 1; }
 // only tex
 __host__ __device__ constexpr int lds_spec_doubles(int mmax, bool spec) { return spec ? 6 * lds_rs(mmax) : 0; }
 __host__ __device__ constexpr int lds_words(int mmax, bool spec) { return ((spec ? 6 : 1) * mmax + 3) / 4 * 4; }
-size_t lm_dyn_lds_bytes(int mmax, int nc_max, bool spec);
+// bilinear cell memo (fmpnp_lm_impl.h eval_pass_bil): per point the Bernstein coefficients of
+// the six channel sums as functions of the position inside the point's 2x2 cell, memo[BIL_NB][rs]
+// doubles after the partials.  It bounds a workgroup to BIL_MAX_M points (four 64-point blocks).
+constexpr int BIL_NB = 54;
+constexpr int BIL_MAX_M = 256;
+size_t lm_dyn_lds_bytes(int mmax, int nc_max, bool spec, bool bil_memo = false);
 
 hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream);
 // LM kernel variants (fmpnp_lm_impl.h): Geman-McClure forward with nearest sampling (the
 // hot path), any loss / mode with nearest sampling, bilinear sampling
 constexpr int VAR_NEAREST = 0, VAR_GM = 1, VAR_BILINEAR = 2;
-// ... and the same two nearest variants on FMPNP_LAYOUT_F maps (fp32 only)
-constexpr int VAR_F_NEAREST = 3, VAR_F_GM = 4;
+// ... and the same two nearest variants on FMPNP_LAYOUT_F maps (fp32 only); bilinear sampling
+// without the cell memo (no_memo = 1: every supported point sampled at every evaluation)
+constexpr int VAR_F_NEAREST = 3, VAR_F_GM = 4, VAR_BIL_DIRECT = 5;
 int lm_variant(const fmpnp_options &o);
 const void *lm_kernel_ptr(int dtype, int wps, bool team, bool ratio, int var);
 

@@ -8,12 +8,13 @@ typedef void (*LmFn)(LaunchArgs);
 template <int WPS, bool TEAM, bool RATIO>
 static LmFn pick_var(int var) {
     if (var == VAR_GM) return lm_kernel<float, WPS, TEAM, RATIO, VAR_GM>;
-    if (var == VAR_BILINEAR) return lm_kernel<float, WPS, TEAM, RATIO, VAR_BILINEAR>;
+    if (var == VAR_BILINEAR) return nullptr;  // the cell memo runs on the WPS_WIDE build only
+    if (var == VAR_BIL_DIRECT) return lm_kernel<float, WPS, TEAM, RATIO, VAR_BIL_DIRECT>;
     if constexpr (WPS == WPS_LATENCY) {  // FMPNP_LAYOUT_F (the planner keeps it on the latency build)
         if (var == VAR_F_GM) return lm_kernel<float, WPS, TEAM, RATIO, VAR_F_GM>;
         if (var == VAR_F_NEAREST) return lm_kernel<float, WPS, TEAM, RATIO, VAR_F_NEAREST>;
     } else {
-        if (var >= VAR_F_NEAREST) return nullptr;
+        if (var == VAR_F_NEAREST || var == VAR_F_GM) return nullptr;
     }
     return lm_kernel<float, WPS, TEAM, RATIO, VAR_NEAREST>;
 }
@@ -25,6 +26,13 @@ static LmFn pick(bool team, bool ratio, int var) {
 
 const void *lm_kernel_ptr_f32(int wps, bool team, bool ratio, int var) {
     // the 128-VGPR throughput build is only planned with G == 1
+    if (wps == WPS_WIDE) {  // the bilinear cell memo only
+        if (var != VAR_BILINEAR) return nullptr;
+        if (team) return ratio ? (const void *)lm_kernel<float, WPS_WIDE, true, true, VAR_BILINEAR>
+                               : (const void *)lm_kernel<float, WPS_WIDE, true, false, VAR_BILINEAR>;
+        return ratio ? (const void *)lm_kernel<float, WPS_WIDE, false, true, VAR_BILINEAR>
+                     : (const void *)lm_kernel<float, WPS_WIDE, false, false, VAR_BILINEAR>;
+    }
     if (wps == WPS_THROUGHPUT) return (const void *)(ratio ? pick_var<WPS_THROUGHPUT, false, true>(var)
                                                            : pick_var<WPS_THROUGHPUT, false, false>(var));
     return (const void *)pick<WPS_LATENCY>(team, ratio, var);

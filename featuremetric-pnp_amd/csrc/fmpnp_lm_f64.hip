@@ -7,9 +7,10 @@ namespace fmpnp {
 typedef void (*LmFn)(LaunchArgs);
 template <int WPS, bool TEAM, bool RATIO>
 static LmFn pick_var(int var) {
-    if (var >= VAR_F_NEAREST) return nullptr;  // FMPNP_LAYOUT_F is fp32-only (validated)
+    if (var == VAR_F_NEAREST || var == VAR_F_GM) return nullptr;  // FMPNP_LAYOUT_F is fp32-only (validated)
     if (var == VAR_GM) return lm_kernel<double, WPS, TEAM, RATIO, VAR_GM>;
-    if (var == VAR_BILINEAR) return lm_kernel<double, WPS, TEAM, RATIO, VAR_BILINEAR>;
+    if (var == VAR_BILINEAR) return nullptr;  // the cell memo runs on the WPS_WIDE build only
+    if (var == VAR_BIL_DIRECT) return lm_kernel<double, WPS, TEAM, RATIO, VAR_BIL_DIRECT>;
     return lm_kernel<double, WPS, TEAM, RATIO, VAR_NEAREST>;
 }
 template <int WPS>
@@ -20,6 +21,13 @@ static LmFn pick(bool team, bool ratio, int var) {
 
 const void *lm_kernel_ptr_f64(int wps, bool team, bool ratio, int var) {
     // the 128-VGPR throughput build is only planned with G == 1
+    if (wps == WPS_WIDE) {  // the bilinear cell memo only
+        if (var != VAR_BILINEAR) return nullptr;
+        if (team) return ratio ? (const void *)lm_kernel<double, WPS_WIDE, true, true, VAR_BILINEAR>
+                               : (const void *)lm_kernel<double, WPS_WIDE, true, false, VAR_BILINEAR>;
+        return ratio ? (const void *)lm_kernel<double, WPS_WIDE, false, true, VAR_BILINEAR>
+                     : (const void *)lm_kernel<double, WPS_WIDE, false, false, VAR_BILINEAR>;
+    }
     if (wps == WPS_THROUGHPUT) return (const void *)(ratio ? pick_var<WPS_THROUGHPUT, false, true>(var)
                                                            : pick_var<WPS_THROUGHPUT, false, false>(var));
     return (const void *)pick<WPS_LATENCY>(team, ratio, var);

@@ -106,6 +106,10 @@ __device__ __forceinline__ double ufirst(double v) {
     const int lo = __builtin_amdgcn_readfirstlane((int)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
+__device__ __forceinline__ unsigned long long ufirst(unsigned long long v) {
+    const unsigned lo = ufirst((unsigned)v), hi = ufirst((unsigned)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
 template <typename P>
 __device__ __forceinline__ P *ufirst(P *p) {
     const uintptr_t b = (uintptr_t)p;
@@ -123,6 +127,7 @@ struct LMState {
     int best_inl, n_evals, n_steps, n_accepted, status, done, has_best, ret_current;
     int abort_flag, sync_ok;
     double wg_max[NT / 64];
+    unsigned long long bil_dirty[BIL_MAX_M / 64];  // bilinear memo: each block's points whose cell changed
     unsigned long long stamp_t[NT / 64], stamp_ph[NT / 64][NSTAMP];  // debug phase stamps (lane 0 per wave)
     Ctx c;
 };
@@ -201,6 +206,8 @@ __device__ __forceinline__ float *lds_qp(int mmax, bool spec) {
 __device__ __forceinline__ double *lds_part(int mmax, bool spec) {
     return reinterpret_cast<double *>(lds_tex(mmax, spec) + lds_words(mmax, spec));
 }
+// the bilinear cell memo memo[BIL_NB][rs] (after part[nc_max][NV]; never with speculation)
+__device__ __forceinline__ double *lds_memo(int mmax, int nc_max) { return lds_part(mmax, false) + (size_t)nc_max * NV; }
 
 // so3exp_map (helpers/utils.py:209-221) and the update R' = dR R, t' = dR t + dt
 // (model.py:416-426).
@@ -793,6 +800,243 @@ __device__ __forceinline__ void gather_bil_block(unsigned long long m, const Tap
     }
 }
 
+// ---------------------------------------------------------------------------
+// Bilinear cell memo (FMPNP_BILINEAR, memoised).  Inside one 2x2 cell a point's sampled
+// vectors are s(ax, ay) = sum_ij u_i(ay) v_j(ax) T_ij with u = (1 - ay, ay), v = (1 - ax, ax),
+// so every channel sum of two sampled vectors is a tensor-product quadratic in (ay, ax):
+//   sum_c A_s B_s = sum_pq b_pq By_p Bx_q,  By = ((1-ay)^2, ay (1-ay), ay^2), Bx likewise,
+// b_00 = <A00,B00>, b_01 = <A00,B01> + <A01,B00>, b_02 = <A01,B01>, b_10 = <A00,B10> + <A10,B00>,
+// b_11 = <A00,B11> + <A01,B10> + <A10,B01> + <A11,B00>, b_12 = <A01,B11> + <A11,B01>,
+// b_20 = <A10,B10>, b_21 = <A10,B11> + <A11,B10>, b_22 = <A11,B11>  (A_ij: row i, column j).
+// The six sums need the pairs (D,D), (X,D), (Y,D), (X,X), (X,Y), (Y,Y) with D_ij = F_ij - fref
+// (e = f_s - fref = sum w D because the weights sum to one): 54 coefficients per point, which
+// depend only on the cell and the point's descriptor.  They are formed once when the point
+// enters a cell (the 2x2 x 3 x C neighbourhood and fref read once, reduced across C in fp64)
+// and kept in LDS; every evaluation inside the cell costs 54 LDS reads and 72 FMAs instead of
+// 52C bytes of taps.  Same sums as sampling first (gather_bil_half) up to fp64 rounding.
+// ---------------------------------------------------------------------------
+// one channel's contributions, symmetric pair (A = B: cross coefficients halved here, doubled
+// after the reduction, exactly)
+__device__ __forceinline__ void bern_sym(double *acc, double a0, double a1, double a2, double a3) {
+    acc[0] = fma(a0, a0, acc[0]);
+    acc[1] = fma(a0, a1, acc[1]);
+    acc[2] = fma(a1, a1, acc[2]);
+    acc[3] = fma(a0, a2, acc[3]);
+    acc[4] = fma(a1, a2, fma(a0, a3, acc[4]));
+    acc[5] = fma(a1, a3, acc[5]);
+    acc[6] = fma(a2, a2, acc[6]);
+    acc[7] = fma(a2, a3, acc[7]);
+    acc[8] = fma(a3, a3, acc[8]);
+}
+__device__ __forceinline__ void bern_asym(double *acc, const double a[4], const double b[4]) {
+    acc[0] = fma(a[0], b[0], acc[0]);
+    acc[1] = fma(a[1], b[0], fma(a[0], b[1], acc[1]));
+    acc[2] = fma(a[1], b[1], acc[2]);
+    acc[3] = fma(a[2], b[0], fma(a[0], b[2], acc[3]));
+    acc[4] = fma(a[3], b[0], fma(a[2], b[1], fma(a[1], b[2], fma(a[0], b[3], acc[4]))));
+    acc[5] = fma(a[3], b[1], fma(a[1], b[3], acc[5]));
+    acc[6] = fma(a[2], b[2], acc[6]);
+    acc[7] = fma(a[3], b[2], fma(a[2], b[3], acc[7]));
+    acc[8] = fma(a[3], b[3], acc[8]);
+}
+// pass 0: (D,D), (X,D), (Y,D); pass 1: (X,X), (X,Y), (Y,Y) -- 27 accumulators each
+constexpr int BIL_PASSES = 2, BIL_PW = 27;
+__device__ __forceinline__ void bern_ch(double acc[BIL_PW], int pass, const double f[4], double r, const double x[4],
+                                        const double y[4]) {
+    if (pass == 0) {
+        const double d[4] = {f[0] - r, f[1] - r, f[2] - r, f[3] - r};  // exact for fp32 texels
+        bern_sym(acc, d[0], d[1], d[2], d[3]);
+        bern_asym(acc + 9, x, d);
+        bern_asym(acc + 18, y, d);
+    } else {
+        bern_sym(acc, x[0], x[1], x[2], x[3]);
+        bern_asym(acc + 9, x, y);
+        bern_sym(acc + 18, y[0], y[1], y[2], y[3]);
+    }
+}
+// Wave-reduce a pass's accumulators and store them into the point's memo column (groups
+// 3 pass .. 3 pass + 2 of the order DD, XD, YD, XX, XY, YY; symmetric: DD, XX, YY).
+__device__ __forceinline__ void bern_store(double acc[BIL_PW], int pass, double *mcol, int rs, int lane) {
+    auto val = [&](int k) -> double { return k < BIL_PW ? acc[k] : 0.0; };
+    const double tot = reduce32_in64(val, lane);
+    const int idx = reduce32_index(lane);
+    if ((lane & 1) == 0 && idx < BIL_PW) {
+        const int g = 3 * pass + idx / 9, c = idx % 9;
+        const bool sym = g == 0 || g == 3 || g == 5;
+        const bool cross = c == 1 || c == 3 || c == 4 || c == 5 || c == 7;
+        mcol[(size_t)(9 * g + c) * rs] = (sym && cross) ? 2.0 * tot : tot;
+    }
+}
+
+// One point's 13 16-byte loads of a lane's channel round (four taps x f, gx, gy, and fref).
+template <typename T>
+struct BilLoad {
+    typename V16<T>::type f[4], x[4], y[4], q;
+};
+template <typename T>
+__device__ __forceinline__ void bil_issue(BilLoad<T> &g, const T *feat, const int o[4], const T *rf, int cs, int c) {
+    using VT = typename V16<T>::type;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const T *t = feat + (size_t)o[k] * 3 * cs + c;
+        g.f[k] = gload<VT>(t);
+        g.x[k] = gload<VT>(t + cs);
+        g.y[k] = gload<VT>(t + 2 * cs);
+    }
+    g.q = gload<VT>(rf + c);
+}
+template <typename T>
+__device__ __forceinline__ void bil_acc(double acc[BIL_PW], int pass, const BilLoad<T> &g) {
+    constexpr int V = V16<T>::n;
+    const T *pq = reinterpret_cast<const T *>(&g.q);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+        double f[4], x[4], y[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            f[k] = (double)reinterpret_cast<const T *>(&g.f[k])[e];
+            x[k] = (double)reinterpret_cast<const T *>(&g.x[k])[e];
+            y[k] = (double)reinterpret_cast<const T *>(&g.y[k])[e];
+        }
+        bern_ch(acc, pass, f, (double)pq[e], x, y);
+    }
+}
+
+// Both passes of one point from one loaded round (C <= 64 V: every lane's channels in one
+// 16-byte round; lanes past the slice read the first vector and contribute zeros).
+template <typename T>
+__device__ __forceinline__ void bil_consume1(const BilLoad<T> &g, bool has, double *mcol, int rs, int lane) {
+#pragma unroll
+    for (int pass = 0; pass < BIL_PASSES; ++pass) {
+        double acc[BIL_PW];
+#pragma unroll
+        for (int k = 0; k < BIL_PW; ++k) acc[k] = 0.0;
+        bil_acc<T>(acc, pass, g);
+        if (!has) {
+#pragma unroll
+            for (int k = 0; k < BIL_PW; ++k) acc[k] = 0.0;
+        }
+        bern_store(acc, pass, mcol, rs, lane);
+    }
+}
+
+// This wave's share of the workgroup's changed cells: the points of bil_dirty[0..nb) in block
+// and lane order, every nw-th one starting at rank w (balanced across the waves whatever the
+// blocks' counts).  Scalar state only.
+struct BilCursor {
+    const unsigned long long *dirty;
+    unsigned long long m;
+    int b, nb, r, w, nwm;  // nwm = nwaves - 1 (a power of two minus one)
+    __device__ __forceinline__ bool next(int &pb, int &pj) {
+        while (true) {
+            while (!m) {
+                if (++b >= nb) return false;
+                m = ufirst(dirty[b]);
+            }
+            const int j = __builtin_ctzll(m);
+            m &= m - 1;
+            if (((r++) & nwm) == w) {
+                pb = b;
+                pj = j;
+                return true;
+            }
+        }
+    }
+};
+
+// The memo columns of this wave's share of the changed cells: one point per trip, the whole
+// wave on its channels; one-round slices keep the next point's loads in flight while the
+// current one is reduced.
+template <typename T>
+__device__ __forceinline__ void bil_memo_build(BilCursor cur, const T *feat, const int *tex, const T *fref0,
+                                               double *memo, int rs, bool vec, int cs, int cb, int ce, int ld, int Hf,
+                                               int Wf) {
+    constexpr int V = V16<T>::n;
+    const int lane = threadIdx.x & 63;
+    int pb, pj;
+    if (vec && ce - cb <= 64 * V) {
+        const int c0 = cb + lane * V;
+        const bool has = c0 < ce;
+        const int c = has ? c0 : cb;
+        BilLoad<T> A, B;
+        int ia = 0, ib = 0;
+        auto issue = [&](BilLoad<T> &g, int &pi) {
+            pi = pb * 64 + pj;
+            int o[4];
+            bil_cell_taps(ufirst(tex[pi]), Hf, Wf, o);
+            bil_issue<T>(g, feat, o, fref0 + (size_t)pi * ld, cs, c);
+        };
+        if (!cur.next(pb, pj)) return;
+        issue(A, ia);
+        while (true) {
+            const bool moreB = cur.next(pb, pj);
+            if (moreB) issue(B, ib);
+            bil_consume1<T>(A, has, memo + ia, rs, lane);
+            if (!moreB) break;
+            const bool moreA = cur.next(pb, pj);
+            if (moreA) issue(A, ia);
+            bil_consume1<T>(B, has, memo + ib, rs, lane);
+            if (!moreA) break;
+        }
+        return;
+    }
+    while (cur.next(pb, pj)) {  // several rounds per lane, or unaligned slices: per pass, rounds in order
+        const int pi = pb * 64 + pj;
+        int o[4];
+        bil_cell_taps(ufirst(tex[pi]), Hf, Wf, o);
+        const T *rf = fref0 + (size_t)pi * ld;
+        const T *t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = feat + (size_t)o[k] * 3 * cs;
+        for (int pass = 0; pass < BIL_PASSES; ++pass) {
+            double acc[BIL_PW];
+#pragma unroll
+            for (int k = 0; k < BIL_PW; ++k) acc[k] = 0.0;
+            if (vec) {
+                for (int c = cb + lane * V; c < ce; c += 64 * V) {
+                    BilLoad<T> g;
+                    bil_issue<T>(g, feat, o, rf, cs, c);
+                    bil_acc<T>(acc, pass, g);
+                }
+            } else {
+                for (int c = cb + lane * V; c < ce; c += 64 * V) {
+#pragma unroll 1
+                    for (int e = 0; e < V; ++e) {
+                        const int ch = c + e;
+                        if (ch < ce) {
+                            double f[4], x[4], y[4];
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                f[k] = (double)t[k][ch];
+                                x[k] = (double)t[k][cs + ch];
+                                y[k] = (double)t[k][2 * cs + ch];
+                            }
+                            bern_ch(acc, pass, f, (double)rf[ch], x, y);
+                        }
+                    }
+                }
+            }
+            bern_store(acc, pass, memo + pi, rs, lane);
+        }
+    }
+}
+
+// The six channel sums of a point at (ax, ay) from its memo column (lane per point).
+__device__ __forceinline__ void bil_memo_sums(const double *mcol, int rs, double ax, double ay, double s[6]) {
+    const double ux = 1.0 - ax, uy = 1.0 - ay;
+    const double bx0 = ux * ux, bx1 = ax * ux, bx2 = ax * ax;
+    const double by0 = uy * uy, by1 = ay * uy, by2 = ay * ay;
+#pragma unroll
+    for (int g = 0; g < 6; ++g) {
+        const double *b = mcol + (size_t)9 * g * rs;
+        const double t0 = fma(b[2 * rs], bx2, fma(b[rs], bx1, b[0] * bx0));
+        const double t1 = fma(b[5 * rs], bx2, fma(b[4 * rs], bx1, b[3 * rs] * bx0));
+        const double t2 = fma(b[8 * rs], bx2, fma(b[7 * rs], bx1, b[6 * rs] * bx0));
+        s[g] = fma(t2, by2, fma(t1, by1, t0 * by0));
+        __builtin_amdgcn_sched_barrier(0);  // nine LDS reads in flight at a time, not 54
+    }
+}
+
 // Double-buffered pair gathers of one block: the next pair's loads are issued before this
 // pair's channel sums are reduced (one exposed round trip per block, not one per pair).
 // fref0: the block's first descriptor row; rd: where the records go.
@@ -1357,6 +1601,102 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
     return lmax;
 }
 
+// One evaluation with bilinear sampling and the cell memo.  The workgroup holds at most four
+// 64-point blocks (the memo's LDS; planner), so wave w < nb owns block w:
+//   A  project its block (lane per point): cell key, (ax, ay), support; ballot the points
+//      whose cell changed into bil_dirty[w];                                    -- barrier
+//   B  every wave builds memo columns: waves w, w + nb, ... share block w mod nb's changed
+//      points (interleaved lanes), one point per trip across the channels;      -- barrier
+//   C  the owner evaluates its points' six sums from the memo, then loss and partials exactly
+//      as eval_pass (rec fields 0..5 hold the sums).
+// The memo columns and the reduction order depend only on the point, so results do not
+// depend on G or on which wave builds a column.
+template <typename T>
+__device__ __forceinline__ double eval_pass_bil(const PC &q, int mmax, long long &ngath) {
+    LMState &st = S();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const double *X = lds_X(mmax);
+    double *rec = lds_rec(mmax);
+    int *tex = lds_tex(mmax, false);
+    double *memo = lds_memo(mmax, q.nc_max);
+    const int rs = lds_rs(mmax);
+    const T *feat = reinterpret_cast<const T *>(q.feat);
+    const T *fref = reinterpret_cast<const T *>(q.fref);
+    constexpr int V = V16<T>::n;
+    const bool vec = ((((uintptr_t)feat) | ((uintptr_t)fref)) & 15) == 0 && q.cs % V == 0 && q.ld % V == 0 &&
+                     q.cb % V == 0 && (q.ce - q.cb) % V == 0;
+    double *dst_g = q.part_g;
+    if (q.G > 1) dst_g += (size_t)((ufirst((int)st.c.epoch) + 1) & 1) * q.nc_max * NV;
+    const int nb = (q.M + 63) >> 6;  // <= BIL_MAX_M / 64 <= nwaves()
+    const bool own = wave < nb;
+    const int i = wave * 64 + lane;
+    const bool valid = own && i < q.M;
+    double Pc[3] = {0.0, 0.0, 1.0};
+    double ax = 0.0, ay = 0.0;
+    int key = -1;
+    if (own) {
+        double Re[9], te[3];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Re[k] = st.Re[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) te[k] = st.te[k];
+        const int old = valid ? tex[i] : -1;
+        if (valid) {
+            transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
+            int x, y;
+            double qx, qy;
+            if (project_px(q.K, Pc, q.im_w, q.im_h, x, y, qx, qy)) {
+                Taps tp;
+                bilinear_taps(qx, qy, q.Hf, q.Wf, q.im_w, q.im_h, tp);
+                key = tp.key;
+                ax = tp.ax;
+                ay = tp.ay;
+            }
+            tex[i] = key;
+        }
+        const unsigned long long m = __ballot(key >= 0 && key != old);
+        ngath += __popcll(m);
+        if (lane == 0) st.bil_dirty[wave] = m;
+    }
+    dbg_stamp(q.stamps, 0);
+    __syncthreads();
+    {
+        // every wave takes every nwaves()-th changed cell of the workgroup (ranks in block order);
+        // wave 0, which runs the LM tail after the barrier, takes the last residue
+        const int nwm = nwaves() - 1;
+        const BilCursor cur{st.bil_dirty, ufirst(st.bil_dirty[0]), 0, nb, 0, (wave + nwm) & nwm, nwm};
+        bil_memo_build<T>(cur, feat, tex, fref + (size_t)q.p0 * q.ld, memo, rs, vec, q.cs, q.cb, q.ce, q.ld, q.Hf,
+                          q.Wf);
+    }
+    dbg_stamp(q.stamps, 1);
+    __syncthreads();
+    double lmax = -1.0;
+    if (own) {
+        const bool sup = key >= 0;
+        const int ii = valid ? i : 0;
+        if (sup) {
+            double s6[6];
+            bil_memo_sums(memo + ii, rs, ax, ay, s6);
+#pragma unroll
+            for (int k = 0; k < 6; ++k) rec[k * rs + ii] = s6[k];
+        }
+        const double *r = rec + ii;
+        double rho = 0.0, d1 = 0.0;
+        if (sup) loss_eval(q.loss, q.alpha, 0.5 * r[0], rho, d1);
+        if (q.use_ratio) {
+            if (valid) {
+                rec[6 * rs + i] = rho;
+                rec[7 * rs + i] = d1;
+            }
+            if (sup) lmax = nanmax(lmax, fabs(rho));
+        } else {
+            contrib_block(q, mmax, wave, sup, sup, rho, d1, r, rs, Pc, dst_g);
+        }
+    }
+    dbg_stamp(q.stamps, 2);
+    return lmax;
+}
+
 // Second pass of the ratio test: the weights of points with |rho| >= max|rho| * thr
 // are zero (model.py:324-336); P is recomputed bit-identically from X.
 __device__ __forceinline__ void contrib_pass(const PC &q, int mmax) {
@@ -1704,7 +2044,7 @@ __device__ __forceinline__ void lm_update_wave(double tot, bool stamps) {
 // VAR_NEAREST (any loss / mode, nearest) or VAR_BILINEAR -- constant-folding the other
 // paths out shortens the per-point code and frees registers.
 template <typename T, int WPS, bool TEAM, bool RATIO, int VAR>
-__global__ __launch_bounds__(WPS == WPS_THROUGHPUT ? NT_THROUGHPUT : NT, 2) void lm_kernel(LaunchArgs a) {
+__global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS_WIDE ? 1 : 2) void lm_kernel(LaunchArgs a) {
     LMState &st = S();
     const int G = a.G;
     // XCD-aware team placement: members of one team share blockIdx % gw (the same XCD
@@ -1755,14 +2095,20 @@ __global__ __launch_bounds__(WPS == WPS_THROUGHPUT ? NT_THROUGHPUT : NT, 2) void
         PC q = load_pc();
         if constexpr (!TEAM) q.G = 1;
         q.use_ratio = RATIO ? 1 : 0;
+        // speculation: the nearest-sampling variants of the latency build
+        constexpr bool kSpec = kSpecBuild && VAR != VAR_BILINEAR && VAR != VAR_BIL_DIRECT && WPS == WPS_LATENCY;
         if constexpr (VAR == VAR_GM || VAR == VAR_F_GM) q.loss = FMPNP_GEMAN_MCCLURE;
-        q.bilinear = VAR == VAR_BILINEAR ? 1 : 0;
+        q.bilinear = (VAR == VAR_BILINEAR || VAR == VAR_BIL_DIRECT) ? 1 : 0;
         long long ngath = 0;  // texel gathers of this wave for this problem
         while (!st.done) {
             // project, gather, loss (+ partials)
             // (double-buffered gathers in both builds; speculation in the latency build only)
-            const double lmax = eval_pass<T, true, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST),
-                                          kSpecBuild && VAR != VAR_BILINEAR && WPS == WPS_LATENCY>(q, mmax, ngath);
+            // (bilinear: the cell memo; VAR_BIL_DIRECT samples every point at every evaluation)
+            double lmax;
+            if constexpr (VAR == VAR_BILINEAR)
+                lmax = eval_pass_bil<T>(q, mmax, ngath);
+            else
+                lmax = eval_pass<T, true, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST), kSpec>(q, mmax, ngath);
             if (q.use_ratio) {
                 if (!ratio_exchange(lmax)) break;
                 contrib_pass(q, mmax);
@@ -1773,7 +2119,7 @@ __global__ __launch_bounds__(WPS == WPS_THROUGHPUT ? NT_THROUGHPUT : NT, 2) void
             constexpr bool FLV = VAR == VAR_F_GM || VAR == VAR_F_NEAREST;
             const bool held = !FLV && WPS == WPS_LATENCY && spec_vec1<T>(q);
             SpecHold<T> hold;
-            if (kSpecBuild && VAR != VAR_BILINEAR && WPS == WPS_LATENCY && q.spec && tid < 64) {
+            if (kSpec && q.spec && tid < 64) {
                 if (held) spec0_issue<T>(q, mmax, hold);
                 else spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath);
                 dbg_stamp(q.stamps, 12);  // wave 0's own speculation (before the barrier)
@@ -1787,12 +2133,12 @@ __global__ __launch_bounds__(WPS == WPS_THROUGHPUT ? NT_THROUGHPUT : NT, 2) void
                     dbg_stamp(q.stamps, 4);
                     lm_update_wave(tot, q.stamps);
                 }
-                if (kSpecBuild && VAR != VAR_BILINEAR && WPS == WPS_LATENCY && q.spec && held) {
+                if (kSpec && q.spec && held) {
                     if (q.ce - q.cb == 64 * V16<T>::n) spec0_finish<T, true>(q, mmax, hold, ngath);
                     else spec0_finish<T, false>(q, mmax, hold, ngath);
                     spec_pass<T, true, false>(q, mmax, ngath, nwaves());  // wave 0's further blocks
                 }
-            } else if (kSpecBuild && VAR != VAR_BILINEAR && WPS == WPS_LATENCY && q.spec) {
+            } else if (kSpec && q.spec) {
                 // the other waves gather their blocks' predicted next texels meanwhile
                 spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath);
                 dbg_stamp(q.stamps, 4);  // waves >= 1: the speculative gathers

@@ -136,6 +136,11 @@ def stream_ptr(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+def spec_build():
+    """True when libfmpnp.so was built with the speculative next-texel gathers (-DFMPNP_SPEC=1)."""
+    return b"speculative_gathers=1" in load().fmpnp_build_info()
+
+
 def last_launch():
     v = [ctypes.c_int() for _ in range(4)]
     load().fmpnp_last_launch(*[ctypes.byref(x) for x in v])

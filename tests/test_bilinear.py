@@ -145,3 +145,86 @@ def test_bilinear_independent_of_workgroups_per_problem():
     for g in (2, 4):
         r = _gpu_case("gm_c16", torch.float64, wgs=g)[0]
         assert np.array_equal(r["R"], base["R"]) and np.array_equal(r["t"], base["t"])
+
+
+# ---------------------------------------------------------------------------
+# The cell memo (fmpnp_lm_impl.h eval_pass_bil): the default bilinear path keeps each point's
+# 54 Bernstein coefficients per 2x2 cell and re-forms the six channel sums from them while the
+# point stays in its cell; no_memo = 1 (VAR_BIL_DIRECT) samples every point at every evaluation.
+# The two are the same sums up to fp64 rounding, so the fp64 tolerances of the oracle tests hold.
+# ---------------------------------------------------------------------------
+def _gpu_run(prob, iters, lambda0, loss, ratio, dtype_code, memo, wgs=0):
+    from fmpnp import refine as rf
+    opts = rf.make_options(iters, lambda0, loss, 0.0, ratio, dtype_code, wgs_per_problem=wgs, sampling="bilinear",
+                           memoize=memo)
+    (res,), (tr,) = rf.refine([prob], opts, trace=True)
+    return res, tr
+
+
+@gpu
+@pytest.mark.parametrize("name", ["gm_c16", "cauchy_c16", "ratio08_gm", "odd_geom_gm", "behind_camera_gm"])
+def test_bilinear_memo_matches_direct_sampling(name):
+    import torch
+    from fmpnp import _lib, refine as rf
+    inp, meta, _ = case(name)
+    f, gx, gy = maps64(inp, orc.sobel)
+    feats = rf.pack_features(torch.from_numpy(f), torch.from_numpy(gx), torch.from_numpy(gy), storage=torch.float64,
+                             device="cuda:0")
+    prob = rf.make_problem(feats, torch.from_numpy(inp["fref"]), inp["pts3d"], inp["K"], inp["im_width"],
+                           inp["im_height"], inp["R0"], inp["t0"])
+    loss = {"geman_mcclure": _lib.GEMAN_MCCLURE, "cauchy": _lib.CAUCHY, "squared": _lib.SQUARED}[meta["loss"]]
+    args = (prob, meta["n_iters"], meta["lambda0"], loss, meta.get("ratio_threshold"), feats.dtype_code)
+    a, ta = _gpu_run(*args, memo=True)
+    b, tb = _gpu_run(*args, memo=False)
+    assert a["status"] == b["status"] and a["n_evals"] == b["n_evals"]
+    np.testing.assert_array_equal(ta["n_supported"], tb["n_supported"])
+    np.testing.assert_allclose(ta["cost"], tb["cost"], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(a["R"], b["R"], atol=1e-11)
+    np.testing.assert_allclose(a["t"], b["t"], atol=1e-11)
+    # the memo gathers a cell once; direct sampling reads every supported point every evaluation
+    assert a["texel_gathers"] <= b["texel_gathers"]
+
+
+def _synthetic_bilinear(N, C, Hf, Wf, seed, init, c_begin=0, c_end=None, iters=50, wgs=0, memo=True):
+    """fp32 packed maps of a synthetic query, the GPU bilinear run, and the oracle's run of
+    the same inputs (fp64 CHW maps = the fp32 map exactly, fp64 Sobel)."""
+    import torch
+    from fmpnp import _lib, refine as rf, synth
+    inp = synth.problem_inputs(N, C, Hf, Wf, seed=seed, device="cuda:0", init=init)
+    feats = rf.pack_features(inp["fmap"], storage=torch.float32, device="cuda:0")
+    prob = rf.make_problem(feats, inp["fref"], inp["pts3d"], inp["K"], inp["im_width"], inp["im_height"],
+                           inp["R0"], inp["t0"], c_begin=c_begin, c_end=c_end)
+    res, tr = _gpu_run(prob, iters, 0.01, _lib.GEMAN_MCCLURE, None, _lib.F32, memo, wgs)
+    fm = inp["fmap"].double().cpu().numpy()
+    gx, gy = orc.sobel(fm)
+    p = orc.make_problem(inp["pts3d"], inp["fref"].double().cpu().numpy(), fm, gx, gy, inp["K"], inp["im_width"],
+                         inp["im_height"], inp["R0"], inp["t0"], c_begin=c_begin, c_end=c_end)
+    ores, otr = orc.forward(p, orc.make_options(iters, 0.01, "geman_mcclure", sampling="bilinear"), iters + 1)
+    return res, tr, ores, otr
+
+
+def _rot(Ra, Rb):
+    c = (np.trace(np.asarray(Ra).T @ np.asarray(Rb)) - 1.0) / 2.0
+    return math.acos(max(-1.0, min(1.0, c)))
+
+
+@gpu
+@pytest.mark.parametrize("shape,init,slc", [((512, 256, 240, 320), "easy", None),
+                                            ((512, 256, 240, 320), "hard", None),
+                                            ((256, 512, 60, 80), "hard", None),
+                                            ((300, 256, 60, 80), "hard", (1, 203))])
+def test_bilinear_memo_50_iters_against_oracle(shape, init, slc):
+    """The bench's bilinear leg (cfg2 shape, fp32 texels, memo) for the full 50 iterations
+    against the oracle's bilinear restatement; C = 512 takes the memo build's multi-round
+    path, an unaligned channel slice its scalar path.  North-star tolerance on the pose,
+    identical per-evaluation support counts, costs within 1e-6 (fp32 packed gradients)."""
+    N, C, Hf, Wf = shape
+    cb, ce = slc if slc else (0, None)
+    res, tr, ores, otr = _synthetic_bilinear(N, C, Hf, Wf, seed=7, init=init, c_begin=cb, c_end=ce)
+    assert res["status"] == 0 and res["n_evals"] == ores["n_evals"]
+    np.testing.assert_array_equal(tr["n_supported"], otr["n_supported"])
+    np.testing.assert_allclose(tr["cost"], otr["cost"], rtol=1e-6)
+    assert _rot(res["R"], ores["R"]) < 1e-4
+    assert np.linalg.norm(res["t"] - ores["t"]) < 1e-4
+    # cells are re-gathered only when a point changes cell
+    assert res["texel_gathers"] < 0.5 * N * res["n_evals"]

@@ -15,7 +15,9 @@ for q in range(B):
     feats = rf.pack_features(inp["fmap"], storage=torch.float32, device=dev, layout=layout)
     probs.append(rf.make_problem(feats, inp["fref"], inp["pts3d"], inp["K"], inp["im_width"], inp["im_height"], inp["R0"], inp["t0"]))
 spec = os.environ.get("SPEC", "1") == "1"
-opts = rf.make_options(50, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32, wgs_per_problem=wgs, speculate=spec)
+sampling = os.environ.get("SAMPLING", "nearest")  # bilinear: phases 0/1/2 = project / memo build / sums+loss+contrib
+opts = rf.make_options(50, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32, wgs_per_problem=wgs, speculate=spec,
+                       sampling=sampling, memoize=os.environ.get("MEMO", "1") == "1")
 ab = rf.AsyncBatch(probs, opts)
 ab.launch(); torch.cuda.synchronize()
 L = _lib.load()

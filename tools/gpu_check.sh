@@ -1,12 +1,9 @@
 #!/bin/bash
-# GPU check: smoke + GPU parity tests (run via gpurun from the repo root).
+# Full GPU test suite, smoke, and a short default bench line.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-.}"
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
-rocminfo 2>/dev/null | grep -m4 -E "gfx950|Marketing Name" > gpurun_out/rocminfo.txt
-timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed rc=$?"; tail -30 gpurun_out/smoke.log; exit 1; }
-tail -2 gpurun_out/smoke.log
-timeout -k 10 700 python -m pytest tests/ -x -q -m gpu ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
-rc=$?
-tail -30 gpurun_out/pytest_gpu.log
-exit $rc
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
