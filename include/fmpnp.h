@@ -54,7 +54,8 @@ typedef enum {
 
 typedef enum {
     FMPNP_NEAREST = 0,   /* the reference: round(K P / z) - 1, floor rescale (model.py:88-89,306-308) */
-    FMPNP_BILINEAR = 1   /* extension: 2x2 bilinear taps of f, gx, gy */
+    FMPNP_BILINEAR = 1   /* extension: 2x2 bilinear taps of f, gx, gy; the map must have
+                            Hf < 32768 and Wf < 65535 (FMPNP_ETOOBIG otherwise) */
 } fmpnp_sampling;
 
 typedef enum { FMPNP_F32 = 0, FMPNP_F64 = 1 } fmpnp_dtype;
@@ -99,9 +100,12 @@ typedef struct {
     int max_teams;          /* cap on concurrently resident problem teams; 0 = auto */
     int no_memo;            /* 1: re-gather every point's texel at every evaluation (the
                                reference's data movement); 0 (default): re-gather only points
-                               whose texel changed, and gather the texels that points are
-                               predicted to move to next beside the LM tail (speculation);
-                               2: memoised without speculation -- all bit-identical results */
+                               whose texel changed (with a -DFMPNP_SPEC=1 build, also gather the
+                               texels points are predicted to move to next beside the LM tail);
+                               2: memoised without speculation -- all bit-identical results.
+                               FMPNP_BILINEAR: 0/2 keep each point's cell memo (the six sums as
+                               quadratics over its 2x2 cell, rebuilt when the cell changes; same
+                               sums up to fp64 rounding), 1 samples every point every evaluation */
     int layout;             /* fmpnp_layout of every problem's feat */
     int sobel_flags;        /* FMPNP_LAYOUT_F: bit 0 normalized (/8), bit 1 replicate padding
                                (the flags fmpnp_pack_features would have been given) */
