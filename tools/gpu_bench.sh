@@ -1,8 +1,7 @@
 #!/bin/bash
-# GPU bench: short bench.py run (+ optional rocprofv3 kernel stats), from the repo root.
+# The default bench line (what the driver runs), kept as JSON under gpurun_out/.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-.}"
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
-timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?
-tail -5 gpurun_out/bench.err; cat gpurun_out/bench.json
-exit $rc
+timeout -k 10 600 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
+tail -c 600 gpurun_out/bench.json
