@@ -1664,7 +1664,7 @@ __device__ __forceinline__ double eval_pass_bil(const PC &q, int mmax, long long
         // every wave takes every nwaves()-th changed cell of the workgroup (ranks in block order);
         // wave 0, which runs the LM tail after the barrier, takes the last residue
         const int nwm = nwaves() - 1;
-        const BilCursor cur{st.bil_dirty, ufirst(st.bil_dirty[0]), 0, nb, 0, (wave + nwm) & nwm, nwm};
+        const BilCursor cur{st.bil_dirty, nb > 0 ? ufirst(st.bil_dirty[0]) : 0ull, 0, nb, 0, (wave + nwm) & nwm, nwm};
         bil_memo_build<T>(cur, feat, tex, fref + (size_t)q.p0 * q.ld, memo, rs, vec, q.cs, q.cb, q.ce, q.ld, q.Hf,
                           q.Wf);
     }

@@ -106,3 +106,34 @@ def test_mixed_sizes_in_one_batch_match_single_launches():
         (r1,), _ = rf.refine([p], opts)
         assert np.array_equal(r1["R"], rb["R"]) and np.array_equal(r1["t"], rb["t"])
         assert r1["best_cost"] == rb["best_cost"] or (math.isnan(r1["best_cost"]) and math.isnan(rb["best_cost"]))
+
+
+def _bil_problem(inp, feats, n):
+    pts, fref = inp["pts3d"][:n], inp["fref"][:n]
+    return rf.make_problem(feats, torch.from_numpy(fref.reshape(n, -1) if n else np.zeros((0, fref.shape[1]))),
+                           pts.reshape(n, 3), inp["K"], inp["im_width"], inp["im_height"], inp["R0"], inp["t0"])
+
+
+def test_bilinear_memo_one_team_walks_mixed_sizes():
+    """The bilinear cell memo keeps per-workgroup state (the dirty ballots, the memo columns)
+    from one problem to the next: one team (max_teams = 1) walking problems of 0, 1, all and
+    65 points -- the empty one right after a full one -- gives each problem's own results,
+    equal to its single launch and, for the non-empty ones, to the oracle."""
+    inp, meta, f, gx, gy, feats = packed_case("gm_c16")
+    N = inp["pts3d"].shape[0]
+    sizes = [N, 0, 1, N, 65 if N > 65 else N - 1]
+    probs = [_bil_problem(inp, feats, n) for n in sizes]
+    opts = dict(dtype=_lib.F64, sampling="bilinear")
+    res, _ = rf.refine(probs, rf.make_options(12, 0.01, _lib.GEMAN_MCCLURE, max_teams=1, **opts))
+    for n, p, r in zip(sizes, probs, res):
+        (single,), _ = rf.refine([p], rf.make_options(12, 0.01, _lib.GEMAN_MCCLURE, **opts))
+        assert np.array_equal(r["R"], single["R"]) and np.array_equal(r["t"], single["t"]), n
+        assert r["status"] == single["status"], n
+        if n == 0:
+            assert r["status"] == _lib.STATUS_NO_SUPPORT
+            continue
+        op = orc.make_problem(inp["pts3d"][:n], inp["fref"][:n], f, gx, gy, inp["K"], inp["im_width"],
+                              inp["im_height"], inp["R0"], inp["t0"])
+        ores, _ = orc.forward(op, orc.make_options(12, 0.01, "geman_mcclure", sampling="bilinear"))
+        np.testing.assert_allclose(r["R"], ores["R"], atol=1e-9)
+        np.testing.assert_allclose(r["t"], ores["t"], atol=1e-9)
