@@ -43,7 +43,7 @@ def _streams(device):
 
 class RefinePipeline:
     def __init__(self, image_shape=None, storage=torch.float32, device=None, depth=2, model_kwargs=None,
-                 sampling="nearest", layout=None):
+                 sampling="nearest", layout=None, wgs_per_problem=1):
         cfg = config.adapter_kwargs()
         self.image_shape = tuple(image_shape or cfg.get("image_shape", (1024, 1024)))
         self.storage = storage
@@ -52,8 +52,12 @@ class RefinePipeline:
         kw = config.model_kwargs()
         kw.update(model_kwargs or {})
         loss_code, alpha = _losses.resolve(kw["loss_fn"])
+        # one workgroup per query by default: the LM launch then leaves the other CUs to the next
+        # batch's pack and gather on the prep stream, and no workgroup of a launch ever waits on
+        # another that a concurrent kernel could keep from being resident
         self.options = _rf.make_options(kw["n_iters"], kw["lambda_"], loss_code, alpha, kw.get("ratio_threshold"),
-                                        _rf._dtype_code(storage), sampling=sampling)
+                                        _rf._dtype_code(storage), sampling=sampling,
+                                        wgs_per_problem=int(wgs_per_problem))
         self.sampling = sampling
         self.depth = max(1, int(depth))
         # "f" (f plane only, gradients formed in the LM gather) wherever it applies: fp32
