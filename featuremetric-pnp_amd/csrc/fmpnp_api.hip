@@ -369,10 +369,15 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
         static const int dbg = [] { const char *e = getenv("FMPNP_DBG"); return e ? atoi(e) : 0; }();
         a.dbg = dbg;
     }
-    hipError_t e = hipMemsetAsync(a.counters, 0, P.ws_counters, s);
-    if (e != hipSuccess) return (int)e;
-    e = hipMemsetAsync(results_dev, 0, sizeof(fmpnp_result) * (size_t)n, s);  // texel_gathers accumulate
-    if (e != hipSuccess) return (int)e;
+    // teams of G > 1 workgroups count their arrivals and add their texel gathers into zeroed
+    // memory; with G = 1 the kernel writes every result field itself and nothing is zeroed
+    hipError_t e = hipSuccess;
+    if (P.G > 1) {
+        e = hipMemsetAsync(a.counters, 0, P.ws_counters, s);
+        if (e != hipSuccess) return (int)e;
+        e = hipMemsetAsync(results_dev, 0, sizeof(fmpnp_result) * (size_t)n, s);  // texel_gathers accumulate
+        if (e != hipSuccess) return (int)e;
+    }
     e = launch_lm(a, opt->dtype, P.grid, (size_t)P.lds, s);
     g_last = P;
     return (int)e;

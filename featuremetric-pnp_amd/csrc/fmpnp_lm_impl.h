@@ -128,6 +128,7 @@ struct LMState {
     int abort_flag, sync_ok;
     double wg_max[NT / 64];
     unsigned long long bil_dirty[BIL_MAX_M / 64];  // bilinear memo: each block's points whose cell changed
+    long long wg_gath[NT / 64];                     // per-wave texel gathers of the problem (G = 1)
     unsigned long long stamp_t[NT / 64], stamp_ph[NT / 64][NSTAMP];  // debug phase stamps (lane 0 per wave)
     Ctx c;
 };
@@ -368,7 +369,7 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
     __syncthreads();
 }
 
-__device__ __forceinline__ void problem_end() {
+__device__ __forceinline__ void problem_end(bool own_gathers) {
     LMState &st = S();
     if (threadIdx.x == 0) {
         if (st.abort_flag) {
@@ -390,6 +391,11 @@ __device__ __forceinline__ void problem_end() {
             r.n_accepted = st.n_accepted;
             r.status = st.status;
             r.has_best = st.has_best;
+            if (own_gathers) {
+                long long g = 0;
+                for (int w = 0; w < nwaves(); ++w) g += st.wg_gath[w];
+                r.texel_gathers = g;
+            }
         }
     }
     __syncthreads();
@@ -2147,11 +2153,18 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
             dbg_stamp(q.stamps, 7);  // pose update + barrier
             if (st.abort_flag) break;
         }
-        // every wave of every team member adds its share (results are zeroed by the launcher)
-        if ((tid & 63) == 0 && ngath)
-            atomicAdd(reinterpret_cast<unsigned long long *>(&a.results[p].texel_gathers),
-                      (unsigned long long)ngath);
-        problem_end();
+        // texel gathers of the problem: a team's members add their waves' counts to the zeroed
+        // result (G > 1); one workgroup sums its waves' counts in LDS and stores the total with
+        // the other result fields (G = 1: the launch needs no memset)
+        if (TEAM) {
+            if ((tid & 63) == 0 && ngath)
+                atomicAdd(reinterpret_cast<unsigned long long *>(&a.results[p].texel_gathers),
+                          (unsigned long long)ngath);
+        } else {
+            if ((tid & 63) == 0) st.wg_gath[tid >> 6] = ngath;
+            __syncthreads();
+        }
+        problem_end(!TEAM);
     }
     if (stamps_on && (tid & 63) == 0)
         for (int k = 0; k < NSTAMP; ++k)

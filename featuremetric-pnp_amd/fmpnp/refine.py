@@ -344,7 +344,7 @@ def results_from_array(arr):
 
 class AsyncBatch:
     """Device-resident descriptors/results/workspace for repeated asynchronous launches
-    (the bench's timed region: nothing but the LM kernel and its counter memset).
+    (the bench's timed region: nothing but the LM kernel, plus two memsets when G > 1).
 
     Built from Problem objects, or (`from_descriptors`) from an fmpnp_problem array the
     caller filled column-wise -- the streamed pipeline's path, no per-query objects."""
