@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--sampling", choices=["nearest", "bilinear"], default="nearest")
     ap.add_argument("--layout", choices=["fgrad", "f"], default="fgrad")
     ap.add_argument("--wgs", type=int, default=0, help="workgroups per query (0 = planner)")
+    ap.add_argument("--event-every", type=int, default=10,
+                    help="bracket every n-th timed launch with HIP events (kernel duration for the roofline)")
     ap.add_argument("--legs", default="all", help="comma list of " + ",".join(LEGS) + ", or all / none")
     ap.add_argument("--cpu-sample", type=int, default=1024, help="problems in the C-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -194,13 +196,21 @@ def main():
     launch = _lib.last_launch()
 
     # ---------------- timed region: exactly K launches ----------------
+    # HIP events bracket every `event_every`-th launch (the per-launch kernel duration of the
+    # roofline); the others run back to back with nothing between them
     stream = torch.cuda.current_stream(dev)  # the stream the launches go to (_lib.stream_ptr)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    every = max(1, args.event_every)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range((args.steps + every - 1) // every)]
 
     def step(k):
-        ev[k][0].record(stream)
+        if k % every:
+            batch.launch()
+            return
+        e0, e1 = ev[k // every]
+        e0.record(stream)
         batch.launch()
-        ev[k][1].record(stream)
+        e1.record(stream)
 
     elapsed = shard.timed_steps(step, args.steps, device=dev)
     kernel_s = float(np.mean([a.elapsed_time(b) for a, b in ev])) / 1e3
@@ -242,6 +252,8 @@ def main():
                        "parallelism": f"query sharding x{world} (no collectives)", "launch": launch},
             "gn_iters_per_s": round(value * ITERS, 1),
             "roofline": roofline(tag, res, kernel_s, B, args.sampling, args.layout),
+            "kernel_timing": f"HIP events on the launch stream around every {every}-th of the {args.steps} timed "
+                             f"launches ({len(ev)} samples)",
             "statuses": statuses,
         }
         out.update(extras)
