@@ -496,3 +496,25 @@ def test_feature_pnp_multi_matches_reference(tag, storage):
     else:
         assert rot_angle(R.numpy(), z[f"out_R_{tag}"]) < 1e-4
         assert np.linalg.norm(t.numpy() - z[f"out_t_{tag}"]) < 1e-4
+
+
+@pytest.mark.parametrize("wgs", [1, 3])
+def test_async_launch_writes_every_result_field(wgs):
+    """With one workgroup per problem the launch zeroes nothing (fmpnp_refine_batch_async):
+    the kernel itself writes every field of every result, texel_gathers included.  The
+    result buffer is filled with 0xFF bytes (NaN doubles, -1 integers) before each launch;
+    the results must equal the synchronous refine's, with G = 1 and with a team (G = 3)."""
+    inputs = synth.problem_inputs(300, 64, 60, 80, seed=78, device=DEV)
+    feats = rf.pack_features(inputs["fmap"], storage=torch.float32, device=DEV)
+    prob = rf.make_problem(feats, inputs["fref"], inputs["pts3d"], inputs["K"], inputs["im_width"],
+                           inputs["im_height"], inputs["R0"], inputs["t0"])
+    opts = rf.make_options(15, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32, wgs_per_problem=wgs)
+    want = rf.refine([prob], opts)[0][0]
+    ab = rf.AsyncBatch([prob] * 4, opts)
+    for _ in range(2):
+        ab.d_res.fill_(255)
+        ab.launch()
+        assert _lib.last_launch()["wgs_per_problem"] == wgs
+        for r in ab.results():
+            for k, v in want.items():
+                assert np.array_equal(np.asarray(r[k]), np.asarray(v), equal_nan=True), k

@@ -25,7 +25,9 @@ while IFS='|' read -r tag flags; do
   B=$(echo "$tag" | sed -E 's/^b([0-9]+)_.*/\1/')
   D="$OUT/$tag"; mkdir -p "$D"
   echo "[profile] $tag: $flags"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/trace" -o run -- python3 "$REPO/bench.py" $BASE --batch $B $flags > "$D/bench.json" 2> "$D/trace.err" || { echo "trace $tag failed"; tail -20 "$D/trace.err"; exit 1; }
+  # the kernel-trace pass runs more launches than the counter passes, so the warm-up launch
+  # barely weighs on the average duration
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/trace" -o run -- python3 "$REPO/bench.py" ${TRACE_BASE:-$BASE} --batch $B $flags > "$D/bench.json" 2> "$D/trace.err" || { echo "trace $tag failed"; tail -20 "$D/trace.err"; exit 1; }
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$D/pmc_fetch" -o run -- python3 "$REPO/bench.py" $BASE --batch $B $flags > /dev/null 2> "$D/pmc_fetch.err" || { echo "fetch $tag failed"; tail -20 "$D/pmc_fetch.err"; exit 1; }
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$D/pmc_write" -o run -- python3 "$REPO/bench.py" $BASE --batch $B $flags > /dev/null 2> "$D/pmc_write.err" || { echo "write $tag failed"; tail -20 "$D/pmc_write.err"; exit 1; }
   python3 "$REPO/tools/pmc_summary.py" "$D" "$B" "$D/summary.json" auto "$tag" || exit 1

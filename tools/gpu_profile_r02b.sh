@@ -10,4 +10,5 @@ b128_easy_bilinear|--sampling bilinear
 b128_easy_nomemo_bilinear|--sampling bilinear --no-memo
 b128_easy_layoutf|--layout f
 b1024_easy|"
+export TRACE_BASE="--legs none --steps 100 --warmup 3 --event-every 1"
 exec "$(dirname "$0")/gpu_profile_r02.sh"
