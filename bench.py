@@ -263,9 +263,10 @@ def main():
         tdist.destroy_process_group()
 
 
-def time_launches(batch, reps, stream):
-    """Mean ms per launch over `reps` back-to-back launches (after one warm-up), results."""
-    batch.launch()
+def time_launches(batch, reps, stream, warmup=1):
+    """Mean ms per launch over `reps` back-to-back launches (after `warmup` launches), results."""
+    for _ in range(warmup):
+        batch.launch()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record(stream)
@@ -388,7 +389,8 @@ def fixed_total_leg(args, dev, probs, feats, inputs, opts, rf, synth, stream):
         ps.append(rf.make_problem(f, inp["fref"], inp["pts3d"], inp["K"], inp["im_width"], inp["im_height"],
                                   inp["R0"], inp["t0"]))
         del inp
-    ms, r = time_launches(rf.AsyncBatch(ps, opts), 5, stream)
+    # (226 GB of freshly allocated maps: the first launches also warm the address translation)
+    ms, r = time_launches(rf.AsyncBatch(ps, opts), 20, stream, warmup=3)
     d = leg_summary(workload_tag(n, args.init, args.ratio, not args.no_memo, args.sampling, layout), ms, r, n,
                     args.sampling, layout)
     d.update(layout=layout, launch=_lib.last_launch(),
