@@ -117,7 +117,8 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     };
     // workgroups per problem: one while the batch covers at least half of the CUs (a
     // team member saves less per evaluation than its cross-workgroup exchange costs:
-    // measured B=128 on 256 CUs, G=1 0.53 ms vs G=2 0.55 ms); smaller batches spread
+    // measured B=128 on 256 CUs, G=1 0.367 ms vs G=2 0.386 ms; per evaluation a lone wave's
+    // point phase is 6.7k cycles either way and the exchange ~3.6k); smaller batches spread
     // each problem so that the teams cover every CU.  Bounded by the chunks of the
     // largest problem and by what fits in LDS at the resulting density.
     int G;
@@ -365,6 +366,14 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
     a.stamps = g_stamps;
     a.wps = P.wps;
     a.spec = P.spec;
+    {
+        // speculative gathers per wave per evaluation (waves >= 1 gather during wave 0's LM tail:
+        // more than fit in it would delay the evaluation's closing barrier)
+        static const int cap = [] { const char *e = getenv("FMPNP_SPEC_CAP"); return e ? atoi(e) : 4; }();
+        a.spec_cap = cap;
+        static const int w0 = [] { const char *e = getenv("FMPNP_SPEC_W0"); return e ? atoi(e) : 4; }();
+        a.spec_w0 = w0;
+    }
     {
         static const int dbg = [] { const char *e = getenv("FMPNP_DBG"); return e ? atoi(e) : 0; }();
         a.dbg = dbg;

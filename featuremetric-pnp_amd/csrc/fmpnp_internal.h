@@ -5,12 +5,14 @@
 
 #include "fmpnp.h"
 
-// Speculative next-texel gathers (fmpnp_lm_impl.h spec_pass): measured, not adopted -- the
-// gathers they take off the evaluation are paid back by the extra per-point work and register
-// pressure (B=128: 0.367 ms with them, 0.365 ms compiled out).  Build with
-// -DFMPNP_SPEC=1 to measure them.
+// Speculative next-texel gathers (fmpnp_lm_impl.h spec_pass), on the later wave of each SIMD
+// only (waves >= spec_w0 = 4) and at most spec_cap = 4 per wave per evaluation: those waves
+// finish their point phase after their SIMD partners, so their changed texels are the ones
+// worth taking off the evaluation, and four gathers fit in wave 0's LM tail (B=128: 0.3526 vs
+// 0.3623 ms per step without them, interleaved A/B; every wave speculating without a cap:
+// 0.367 vs 0.365 -- DESIGN.md §4.1).  Build with -DFMPNP_SPEC=0 to compile them out.
 #ifndef FMPNP_SPEC
-#define FMPNP_SPEC 0
+#define FMPNP_SPEC 1
 #endif
 
 namespace fmpnp {
@@ -47,6 +49,8 @@ struct LaunchArgs {
     unsigned long long *stamps;   // debug: [grid][8 waves][NSTAMP] phase cycle totals, or null
     int wps;                      // occupancy variant (WPS_LATENCY / WPS_THROUGHPUT)
     int spec;                     // speculative next-texel gathers (memoised nearest modes)
+    int spec_cap;                 // at most this many speculative gathers per wave per evaluation
+    int spec_w0;                  // waves >= spec_w0 speculate (the later wave of each SIMD: 4)
     int dbg;                      // debug knob (FMPNP_DBG): bit 0 census only, bit 1 no consume
 };
 

@@ -63,6 +63,8 @@ struct Ctx {
     double lambda0, ratio_thr, alpha;
     int mode, n_iters, use_ratio, loss, G, s, trace_stride, nc_max, no_memo, sampling, sobel_flags;
     int spec;             // speculative gathers of the predicted next texels (memoised nearest modes)
+    int spec_cap;         // ... at most this many per wave per evaluation
+    int spec_w0;          // ... by the waves >= spec_w0
     int dbg;
     unsigned epoch;       // exchanges done by this team in this launch
     int dead;             // a team exchange timed out: finish remaining problems as failed
@@ -87,6 +89,8 @@ struct PC {
     UDiv dh, dw;
     int loss, no_memo, use_ratio, bilinear;
     int spec;               // speculative next-texel gathers on (runtime: launch option)
+    int spec_cap;           // speculative gathers per wave per evaluation
+    int spec_w0;            // the first wave that speculates
     int dbg;
     float txpx, typx, pxtx, pypx;  // texels per image pixel and image pixels per texel (x, y)
     int sob_norm, sob_rep;  // FMPNP_LAYOUT_F: the in-gather Sobel's flags
@@ -152,6 +156,8 @@ __device__ __forceinline__ PC load_pc() {
     q.loss = ufirst(c.mode == FMPNP_MODE_COMPUTE_COST ? (int)FMPNP_SQUARED : c.loss);
     q.no_memo = ufirst(c.no_memo);
     q.spec = ufirst(c.spec);
+    q.spec_cap = ufirst(c.spec_cap);
+    q.spec_w0 = ufirst(c.spec_w0);
     q.dbg = ufirst(c.dbg);
     q.txpx = (float)q.Wf / (float)q.im_w;
     q.typx = (float)q.Hf / (float)q.im_h;
@@ -1354,10 +1360,15 @@ __device__ __forceinline__ int spec_target(const PC &q, double qx, double qy, in
 // Every wave for its own blocks (wave 0 before the evaluation's barrier, in the slack it has
 // while the later waves of its SIMDs finish; waves 1..7 after it, beside wave 0's LM tail):
 // gather the predicted texels into each point's idle slot, which then holds tex2.
+// At most `budget` gathers per call (q.spec_cap; 0 for wave 0's further blocks): a prediction
+// left out is withdrawn (spec = -1), so the next evaluation gathers that point on demand if
+// it does move there.
 template <typename T, bool PIPE, bool FL>
-__device__ __forceinline__ void spec_pass(const PC &q, int mmax, long long &ngath, int first_blk = -1) {
+__device__ __forceinline__ void spec_pass(const PC &q, int mmax, long long &ngath, int first_blk = -1,
+                                          int budget = 1 << 30) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int *tex = lds_tex(mmax, true), *spec = lds_spec(mmax, true), *slot = lds_slot(mmax, true);
+    int *spec_w = lds_spec(mmax, true);
+    const int *tex = lds_tex(mmax, true), *spec = spec_w, *slot = lds_slot(mmax, true);
     const int *tex2 = lds_tex2(mmax, true);
     double *rec = lds_rec(mmax), *rec2 = lds_rec2(mmax);
     const int rs = lds_rs(mmax);
@@ -1370,8 +1381,19 @@ __device__ __forceinline__ void spec_pass(const PC &q, int mmax, long long &ngat
         const int ii = valid ? i : 0;
         const int sp = valid ? spec[ii] : -1, cur = tex[ii], t2 = tex2[ii], sl = slot[ii];
         const bool want = sp >= 0 && sp != cur && sp != t2;
-        const unsigned long long m = __ballot(want);
+        unsigned long long m = __ballot(want);
         if (!m) continue;
+        {
+            unsigned long long kept = 0, mm = m;
+            for (int k = 0; k < budget && mm; ++k) {
+                kept |= mm & (~mm + 1);
+                mm &= mm - 1;
+            }
+            budget -= __popcll(kept);
+            if (valid && ((m & ~kept) >> lane) & 1ull) spec_w[i] = -1;  // not gathered: withdrawn
+            m = kept;
+            if (!m) continue;
+        }
         ngath += __popcll(m);
         int rc = 0;
         if (FL && want) rc = ((sp / q.Wf) << 16) | (sp % q.Wf);
@@ -1428,7 +1450,10 @@ __device__ __forceinline__ void spec0_issue(const PC &q, int mmax, SpecHold<T> &
     };
     h.a0 = take();
     h.a1 = take();
-    h.rest = m;
+    // the held pair only: wave 0 gathers nothing else after its tail (further predictions of
+    // its block are withdrawn; the next evaluation gathers those points on demand)
+    if (valid && (m >> lane) & 1ull) lds_spec(mmax, true)[lane] = -1;
+    h.rest = 0;
     h.any = h.a0.j >= 0;
     if (!h.any) return;
     const T *feat = reinterpret_cast<const T *>(q.feat);
@@ -1497,7 +1522,8 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
     const bool vec = ((((uintptr_t)feat) | ((uintptr_t)fref)) & 15) == 0 && cs % V == 0 && ld % V == 0 &&
                      cb % V == 0 && (ce - cb) % V == 0;
     const bool defer = q.use_ratio != 0;
-    const bool spec_on = SP && q.spec != 0;
+    // (a wave below spec_w0 keeps slot 0 and no predictions: the memoised path)
+    const bool spec_on = SP && q.spec != 0 && wave >= q.spec_w0;
     int *tex2 = lds_tex2(mmax, true), *spec = lds_spec(mmax, true), *slot = lds_slot(mmax, true);
     float *qp = lds_qp(mmax, true);
     double *rec2 = lds_rec2(mmax);
@@ -2080,10 +2106,12 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
         c.loss = a.opt.loss;
         c.no_memo = a.opt.no_memo == 1;  // 2: memoised without speculation (a.spec = 0)
         c.spec = a.spec;
+        c.spec_cap = a.spec_cap;
+        c.spec_w0 = a.spec_w0;
         c.dbg = a.dbg;
         c.sampling = a.opt.sampling;
         c.sobel_flags = a.opt.sobel_flags;
-        c.stamps_on = a.stamps != nullptr;
+        c.stamps_on = a.stamps != nullptr && !(a.dbg & 4);  // dbg bit 2: per-evaluation stamps instead
         c.G = G;
         c.s = s;
         c.epoch = 0;
@@ -2091,7 +2119,10 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
     }
     __syncthreads();
     // optional phase stamps (debug: a.stamps != null): s_memtime deltas on thread 0
-    const bool stamps_on = a.stamps != nullptr;
+    const bool stamps_on = a.stamps != nullptr && !(a.dbg & 4);
+    // debug (FMPNP_DBG bit 2): s_memtime at the start of every evaluation of the team's first
+    // problem and after its last, [grid][64] in the stamps buffer
+    unsigned long long *ev_stamps = (a.stamps != nullptr && (a.dbg & 4)) ? a.stamps + (size_t)blockIdx.x * 64 : nullptr;
     if (stamps_on && (tid & 63) == 0) {
         for (int k = 0; k < NSTAMP; ++k) st.stamp_ph[tid >> 6][k] = 0;
         st.stamp_t[tid >> 6] = __builtin_amdgcn_s_memtime();
@@ -2107,6 +2138,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
         q.bilinear = (VAR == VAR_BILINEAR || VAR == VAR_BIL_DIRECT) ? 1 : 0;
         long long ngath = 0;  // texel gathers of this wave for this problem
         while (!st.done) {
+            if (ev_stamps && tid == 0 && p == team && st.n_evals < 63) ev_stamps[st.n_evals] = __builtin_amdgcn_s_memtime();
             // project, gather, loss (+ partials)
             // (double-buffered gathers in both builds; speculation in the latency build only)
             // (bilinear: the cell memo; VAR_BIL_DIRECT samples every point at every evaluation)
@@ -2125,7 +2157,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
             constexpr bool FLV = VAR == VAR_F_GM || VAR == VAR_F_NEAREST;
             const bool held = !FLV && WPS == WPS_LATENCY && spec_vec1<T>(q);
             SpecHold<T> hold;
-            if (kSpec && q.spec && tid < 64) {
+            if (kSpec && q.spec && tid < 64 && q.spec_w0 == 0) {
                 if (held) spec0_issue<T>(q, mmax, hold);
                 else spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath);
                 dbg_stamp(q.stamps, 12);  // wave 0's own speculation (before the barrier)
@@ -2139,20 +2171,21 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
                     dbg_stamp(q.stamps, 4);
                     lm_update_wave(tot, q.stamps);
                 }
-                if (kSpec && q.spec && held) {
+                if (kSpec && q.spec && held && q.spec_w0 == 0) {
                     if (q.ce - q.cb == 64 * V16<T>::n) spec0_finish<T, true>(q, mmax, hold, ngath);
                     else spec0_finish<T, false>(q, mmax, hold, ngath);
-                    spec_pass<T, true, false>(q, mmax, ngath, nwaves());  // wave 0's further blocks
+                    spec_pass<T, true, false>(q, mmax, ngath, nwaves(), 0);  // wave 0's further blocks: withdrawn
                 }
-            } else if (kSpec && q.spec) {
+            } else if (kSpec && q.spec && (int)(tid >> 6) >= q.spec_w0) {
                 // the other waves gather their blocks' predicted next texels meanwhile
-                spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath);
+                spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath, -1, q.spec_cap);
                 dbg_stamp(q.stamps, 4);  // waves >= 1: the speculative gathers
             }
             __syncthreads();
             dbg_stamp(q.stamps, 7);  // pose update + barrier
             if (st.abort_flag) break;
         }
+        if (ev_stamps && tid == 0 && p == team && st.n_evals < 64) ev_stamps[st.n_evals] = __builtin_amdgcn_s_memtime();
         // texel gathers of the problem: a team's members add their waves' counts to the zeroed
         // result (G > 1); one workgroup sums its waves' counts in LDS and stores the total with
         // the other result fields (G = 1: the launch needs no memset)
