@@ -369,10 +369,10 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
     {
         // speculative gathers per wave per evaluation (waves >= 1 gather during wave 0's LM tail:
         // more than fit in it would delay the evaluation's closing barrier)
-        static const int cap = [] { const char *e = getenv("FMPNP_SPEC_CAP"); return e ? atoi(e) : 4; }();
-        a.spec_cap = cap;
-        static const int w0 = [] { const char *e = getenv("FMPNP_SPEC_W0"); return e ? atoi(e) : 4; }();
-        a.spec_w0 = w0;
+        // (read per launch: measurement and test knobs, FMPNP_SPEC_CAP / FMPNP_SPEC_W0)
+        const char *ec = getenv("FMPNP_SPEC_CAP"), *ew = getenv("FMPNP_SPEC_W0");
+        a.spec_cap = ec ? std::max(0, atoi(ec)) : 4;
+        a.spec_w0 = ew ? std::max(0, atoi(ew)) : 4;
     }
     {
         static const int dbg = [] { const char *e = getenv("FMPNP_DBG"); return e ? atoi(e) : 0; }();

@@ -150,3 +150,26 @@ def test_speculative_gathers_change_nothing(layout, init, ratio, wgs):
         np.testing.assert_array_equal(ta["n_supported"], t["n_supported"])
     # speculation reads more texels in total, but the evaluations themselves gather fewer
     assert c["texel_gathers"] >= b["texel_gathers"]
+
+
+@pytest.mark.parametrize("w0,cap", [("0", "4"), ("1", "64"), ("4", "0"), ("4", "2"), ("4", "4"), ("8", "4")])
+def test_speculation_settings_change_nothing(w0, cap, monkeypatch):
+    """Which waves speculate (FMPNP_SPEC_W0: the default 4 is the later wave of each SIMD; 0
+    adds wave 0's held pair; 8 none) and how many texels each gathers per evaluation
+    (FMPNP_SPEC_CAP; a withdrawn prediction is gathered on demand) only move where sums come
+    from: bit-identical to the run without speculation."""
+    if not _lib.spec_build():
+        pytest.skip("library built without speculation")
+    inp = synth.problem_inputs(512, 256, 240, 320, seed=23, device=DEV, init="hard")
+    prob = packed_problem(inp, "fgrad")
+    o = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32, speculate=False)
+    (base,), (tb,) = rf.refine([prob], o, trace=True)
+    monkeypatch.setenv("FMPNP_SPEC_W0", w0)
+    monkeypatch.setenv("FMPNP_SPEC_CAP", cap)
+    o = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32, speculate=True)
+    (r,), (t,) = rf.refine([prob], o, trace=True)
+    assert np.array_equal(base["R"], r["R"]) and np.array_equal(base["t"], r["t"])
+    assert base["best_cost"] == r["best_cost"] and base["n_evals"] == r["n_evals"]
+    np.testing.assert_array_equal(tb["cost"], t["cost"])
+    np.testing.assert_array_equal(tb["n_supported"], t["n_supported"])
+    np.testing.assert_array_equal(tb["lam"], t["lam"])
