@@ -91,8 +91,15 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     // speculative next-texel gathers (fmpnp_lm_impl.h spec_pass): memoised nearest sampling of
     // a forward run; no_memo = 2 keeps the memo without them (a measurement knob)
     // (the f-only layout's nine-texel gathers are too heavy to hide: B=128 0.68 -> 0.75 ms with it)
+    // Only where it pays (measured): every problem's channel slice within one 16-byte round per
+    // half-wave lane (C <= 64 V: 256 fp32 channels; at C = 512 the gathers outgrow wave 0's
+    // tail, 0.437 vs 0.415 ms on the pyramid's coarse level) and, below, one workgroup per
+    // problem on the latency build (a team's waves 4-7 own no block at these sizes).
+    int max_span = 0;
+    for (int i = 0; i < n; ++i) max_span = std::max(max_span, probs[i].c_end - probs[i].c_begin);
     P.spec = (FMPNP_SPEC && opt->no_memo == 0 && opt->sampling == FMPNP_NEAREST &&
-              opt->mode == FMPNP_MODE_FORWARD && opt->layout == FMPNP_LAYOUT_FGRAD) ? 1 : 0;
+              opt->mode == FMPNP_MODE_FORWARD && opt->layout == FMPNP_LAYOUT_FGRAD &&
+              max_span <= 64 * (16 / elem_size(opt->dtype))) ? 1 : 0;
     // bilinear sampling keeps each point's cell memo in LDS (at most BIL_MAX_M points per
     // workgroup) unless no_memo asks for every point sampled every evaluation
     const bool bil_memo = opt->sampling == FMPNP_BILINEAR && opt->no_memo != 1;
@@ -109,7 +116,9 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb,
                                                          lm_kernel_ptr(opt->dtype, P.wps, P.G > 1,
-                                                                       opt->use_ratio != 0, lm_variant(*opt)),
+                                                                       opt->use_ratio != 0,
+                                                                       P.spec ? spec_variant(lm_variant(*opt))
+                                                                              : lm_variant(*opt)),
                                                          P.wps == WPS_LATENCY ? NT : NT_THROUGHPUT, lds) !=
             hipSuccess)
             return 1;
@@ -156,7 +165,7 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     const bool tp = tp_ok && (want == WPS_THROUGHPUT || (want == 0 && (long)n >= 2L * ncu));
     P.wps = tp ? WPS_THROUGHPUT : WPS_LATENCY;
     if (bil_memo) P.wps = WPS_WIDE;  // the memo build's registers: one wave per SIMD
-    if (tp) {
+    if (tp || G > 1) {
         P.spec = 0;
         P.lds = lds_for(G);
     }

@@ -5,7 +5,7 @@
 
 #include "fmpnp.h"
 
-// Speculative next-texel gathers (fmpnp_lm_impl.h spec_pass), on the later wave of each SIMD
+// Speculative next-texel gathers (fmpnp_lm_impl.h spec_pass; variants VAR_*_SPEC), on the later wave of each SIMD
 // only (waves >= spec_w0 = 4) and at most spec_cap = 4 per wave per evaluation: those waves
 // finish their point phase after their SIMD partners, so their changed texels are the ones
 // worth taking off the evaluation, and four gathers fit in wave 0's LM tail (B=128: 0.3526 vs
@@ -78,6 +78,13 @@ constexpr int VAR_NEAREST = 0, VAR_GM = 1, VAR_BILINEAR = 2;
 // ... and the same two nearest variants on FMPNP_LAYOUT_F maps (fp32 only); bilinear sampling
 // without the cell memo (no_memo = 1: every supported point sampled at every evaluation)
 constexpr int VAR_F_NEAREST = 3, VAR_F_GM = 4, VAR_BIL_DIRECT = 5;
+// ... and the two packed nearest variants with the speculative next-texel gathers compiled in
+// (the latency build, one workgroup per problem: the planner's P.spec); the other variants are
+// built without them, so their code does not pay for speculation they do not run
+constexpr int VAR_GM_SPEC = 6, VAR_NEAREST_SPEC = 7;
+inline int spec_variant(int var) {
+    return var == VAR_GM ? VAR_GM_SPEC : var == VAR_NEAREST ? VAR_NEAREST_SPEC : var;
+}
 int lm_variant(const fmpnp_options &o);
 const void *lm_kernel_ptr(int dtype, int wps, bool team, bool ratio, int var);
 

@@ -2133,8 +2133,8 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
         if constexpr (!TEAM) q.G = 1;
         q.use_ratio = RATIO ? 1 : 0;
         // speculation: the nearest-sampling variants of the latency build
-        constexpr bool kSpec = kSpecBuild && VAR != VAR_BILINEAR && VAR != VAR_BIL_DIRECT && WPS == WPS_LATENCY;
-        if constexpr (VAR == VAR_GM || VAR == VAR_F_GM) q.loss = FMPNP_GEMAN_MCCLURE;
+        constexpr bool kSpec = kSpecBuild && (VAR == VAR_GM_SPEC || VAR == VAR_NEAREST_SPEC) && WPS == WPS_LATENCY;
+        if constexpr (VAR == VAR_GM || VAR == VAR_F_GM || VAR == VAR_GM_SPEC) q.loss = FMPNP_GEMAN_MCCLURE;
         q.bilinear = (VAR == VAR_BILINEAR || VAR == VAR_BIL_DIRECT) ? 1 : 0;
         long long ngath = 0;  // texel gathers of this wave for this problem
         while (!st.done) {

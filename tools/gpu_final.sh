@@ -1,14 +1,9 @@
 #!/bin/bash
-# Round evidence: GPU tests, rocprofv3 kernel stats + FETCH/WRITE_SIZE passes (B=128),
-# then the default bench line (which reads the committed traffic summary).
+# End-of-session evidence: the default bench line and every BASELINE config.
 set -o pipefail
-REPO="${GRAFT_REPO_ROOT:-$(pwd)}"
-cd "$REPO"
+cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/ -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
-tail -1 gpurun_out/pytest_gpu.log
-BATCH=128 bash tools/gpu_profile.sh > gpurun_out/profile.log 2>&1 || { echo "profile failed"; tail -30 gpurun_out/profile.log; exit 1; }
-cp gpurun_out/prof/summary.json profiles/pmc_traffic.json  # (on the box; copy it back from gpurun_out/prof/ locally)
-cd "$REPO"
-timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -30 gpurun_out/bench.err; exit 1; }
-cat gpurun_out/bench.json
+timeout -k 10 600 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
+tail -c 300 gpurun_out/bench.json
+timeout -k 10 400 python3 tools/bench_configs.py > gpurun_out/configs.jsonl 2> gpurun_out/configs.err || { tail -20 gpurun_out/configs.err; exit 1; }
+cat gpurun_out/configs.jsonl
