@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 
 #include "fmpnp.h"
@@ -22,8 +23,8 @@ namespace {
 
 struct Plan {
     int G = 1, teams = 1, teams_pad = 8, gw = 8, grid = 8, nc_max = 1, max_n = 0;
-    int mmax = 0, lds = 0, wps = WPS_LATENCY, spec = 0;
-    size_t ws_counters = 0, ws_partials = 0, ws_max = 0, ws_total = 0;
+    int mmax = 0, lds = 0, wps = WPS_LATENCY, spec = 0, helpers = 0, grid_main = 8;
+    size_t ws_counters = 0, ws_partials = 0, ws_max = 0, ws_hrec = 0, ws_hflag = 0, ws_total = 0;
 };
 
 thread_local Plan g_last;
@@ -188,7 +189,26 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     P.ws_counters = align_up((size_t)P.teams_pad * 16 * sizeof(unsigned), 256);
     P.ws_partials = align_up((size_t)P.teams * 2 * P.nc_max * NV * sizeof(double), 256);
     P.ws_max = align_up((size_t)P.teams * 2 * G * sizeof(double), 256);
-    P.ws_total = P.ws_counters + P.ws_partials + P.ws_max;
+    // first-evaluation helpers: with every problem on one resident workgroup and idle CUs left
+    // (grid + n * H <= CUs), H more workgroups per problem gather the initial pose's texels of
+    // its 64-point blocks, so the first evaluation (all N points dirty) is spread over 1 + H
+    // CUs (ms per launch without / with them: B = 1 0.298 / 0.279, B = 8 0.305 / 0.289,
+    // B = 32 0.310 / 0.302, B = 64 0.341 / 0.333); FMPNP_HELPERS=0 switches them off
+    P.grid_main = P.grid;
+    {
+        const char *eh = getenv("FMPNP_HELPERS");
+        const bool on = !eh || atoi(eh) != 0;
+        // (helpers beside the padded main grid, all resident at once: the mains wait on them)
+        const long spare = ((long)ncu - P.grid) / std::max(n, 1);
+        // (the speculating variants carry the hand-off; a single helper per problem -- B > CUs/3 --
+        // measured slower at B = 128: 0.380 vs 0.360 ms, the first evaluation being HBM-bound there)
+        if (on && P.spec && G == 1 && P.wps == WPS_LATENCY && P.teams == n && P.nc_max >= 2 && spare >= 2)
+            P.helpers = (int)std::min<long>(std::min<long>(spare, P.nc_max), 8);
+    }
+    P.grid = P.grid_main + n * P.helpers;
+    P.ws_hrec = P.helpers ? align_up((size_t)n * P.nc_max * CH * HREC * sizeof(double), 256) : 0;
+    P.ws_hflag = P.helpers ? align_up((size_t)n * P.nc_max * sizeof(unsigned long long), 256) : 0;
+    P.ws_total = P.ws_counters + P.ws_partials + P.ws_max + P.ws_hrec + P.ws_hflag;
     *pl = P;
     return 0;
 }
@@ -371,6 +391,16 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
     a.counters = (unsigned *)ws;
     a.partials = (double *)(ws + P.ws_counters);
     a.maxslots = (double *)(ws + P.ws_counters + P.ws_partials);
+    a.helpers = P.helpers;
+    a.grid_main = P.grid_main;
+    a.hrec = (double *)(ws + P.ws_counters + P.ws_partials + P.ws_max);
+    a.hflag = (unsigned long long *)(ws + P.ws_counters + P.ws_partials + P.ws_max + P.ws_hrec);
+    {
+        // flags from earlier launches carry smaller sequence numbers; the magic high bits keep
+        // any other bytes the workspace held from matching
+        static std::atomic<unsigned long long> seq{0};
+        a.htag = 0xF3A9000000000000ull | (++seq & 0xFFFFFFFFFFFFull);
+    }
     a.mmax = P.mmax;
     a.stamps = g_stamps;
     a.wps = P.wps;

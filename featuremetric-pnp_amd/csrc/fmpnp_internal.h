@@ -52,7 +52,15 @@ struct LaunchArgs {
     int spec_cap;                 // at most this many speculative gathers per wave per evaluation
     int spec_w0;                  // waves >= spec_w0 speculate (the later wave of each SIMD: 4)
     int dbg;                      // debug knob (FMPNP_DBG): bit 0 census only, bit 1 no consume
+    // first-evaluation helpers (small batches, one workgroup per problem): workgroups
+    // grid_main .. grid_main + n * helpers - 1 gather the initial pose's records of their
+    // problem's blocks into hrec and publish each block with a tagged flag (lm_kernel)
+    int helpers, grid_main;
+    unsigned long long htag;      // this launch's flag value (a process-wide sequence + a magic)
+    double *hrec;                 // [n][nc_max * CH][HREC] (six sums, then the texel offset)
+    unsigned long long *hflag;    // [n][nc_max]
 };
+constexpr int HREC = 7;
 
 // Fixed LDS head: the LM state + per-problem context (sized generously, 16-B aligned).
 __host__ __device__ constexpr int lds_fixed_bytes() { return 4096; }
@@ -84,6 +92,12 @@ constexpr int VAR_F_NEAREST = 3, VAR_F_GM = 4, VAR_BIL_DIRECT = 5;
 constexpr int VAR_GM_SPEC = 6, VAR_NEAREST_SPEC = 7;
 inline int spec_variant(int var) {
     return var == VAR_GM ? VAR_GM_SPEC : var == VAR_NEAREST ? VAR_NEAREST_SPEC : var;
+}
+// ... and those two with the first-evaluation helpers' hand-off compiled in (small batches:
+// LaunchArgs::helpers; the headline-size batches run without it and without its code)
+constexpr int VAR_GM_SPEC_H = 8, VAR_NEAREST_SPEC_H = 9;
+inline int help_variant(int var) {
+    return var == VAR_GM_SPEC ? VAR_GM_SPEC_H : var == VAR_NEAREST_SPEC ? VAR_NEAREST_SPEC_H : var;
 }
 int lm_variant(const fmpnp_options &o);
 const void *lm_kernel_ptr(int dtype, int wps, bool team, bool ratio, int var);

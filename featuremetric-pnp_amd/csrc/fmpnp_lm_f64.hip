@@ -9,10 +9,12 @@ template <int WPS, bool TEAM, bool RATIO>
 static LmFn pick_var(int var) {
     if (var == VAR_F_NEAREST || var == VAR_F_GM) return nullptr;  // FMPNP_LAYOUT_F is fp32-only (validated)
     if (var == VAR_GM) return lm_kernel<double, WPS, TEAM, RATIO, VAR_GM>;
-    if (var == VAR_GM_SPEC || var == VAR_NEAREST_SPEC) {  // speculation: latency build, one workgroup per problem
-        if constexpr (WPS == WPS_LATENCY && !TEAM) {
+    if (var == VAR_GM_SPEC || var == VAR_NEAREST_SPEC || var == VAR_GM_SPEC_H || var == VAR_NEAREST_SPEC_H) {
+        if constexpr (WPS == WPS_LATENCY && !TEAM) {  // speculation (+ helpers): latency build, G = 1
             if (var == VAR_GM_SPEC) return lm_kernel<double, WPS, TEAM, RATIO, VAR_GM_SPEC>;
-            return lm_kernel<double, WPS, TEAM, RATIO, VAR_NEAREST_SPEC>;
+            if (var == VAR_NEAREST_SPEC) return lm_kernel<double, WPS, TEAM, RATIO, VAR_NEAREST_SPEC>;
+            if (var == VAR_GM_SPEC_H) return lm_kernel<double, WPS, TEAM, RATIO, VAR_GM_SPEC_H>;
+            return lm_kernel<double, WPS, TEAM, RATIO, VAR_NEAREST_SPEC_H>;
         }
         return nullptr;
     }

@@ -91,6 +91,12 @@ struct PC {
     int spec;               // speculative next-texel gathers on (runtime: launch option)
     int spec_cap;           // speculative gathers per wave per evaluation
     int spec_w0;            // the first wave that speculates
+    int helpers;            // first-evaluation helper workgroups per problem (0: none)
+    int hfirst;             // this is the problem's first evaluation
+    int prob;               // the problem's index (helpers' record slots)
+    const double *hrec;     // the helpers' records [n][nc_max * CH][HREC]
+    const unsigned long long *hflag;
+    unsigned long long htag;
     int dbg;
     float txpx, typx, pxtx, pypx;  // texels per image pixel and image pixels per texel (x, y)
     int sob_norm, sob_rep;  // FMPNP_LAYOUT_F: the in-gather Sobel's flags
@@ -1506,7 +1512,7 @@ __device__ __forceinline__ void spec0_finish(const PC &q, int mmax, SpecHold<T> 
 // PIPE: double-buffered gathers (latency variant: the VGPRs for two pairs in flight).
 // SP: the variant can speculate (nearest sampling; bilinear never memoises).
 // ---------------------------------------------------------------------------
-template <typename T, bool PIPE, bool FL, bool SP>
+template <typename T, bool PIPE, bool FL, bool SP, bool HELP>
 __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ngath) {
     LMState &st = S();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1600,6 +1606,35 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         }
         unsigned long long m = __ballot(dirty);
         ngath += __popcll(m);
+        if (HELP && q.hfirst && m) {
+            // first evaluation with helpers: the block's records at the initial pose come from a
+            // helper workgroup (the same gather code at the same pose: identical sums); a point
+            // whose texel the helper saw differently, or a helper that never publishes, is
+            // gathered here as usual
+            const unsigned long long *flag = q.hflag + (size_t)q.prob * q.nc_max + blk;
+            int ok = 1;
+            if (lane == 0) {
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                while (__hip_atomic_load(reinterpret_cast<const g_u64 *>(reinterpret_cast<uintptr_t>(flag)),
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != q.htag) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) { ok = 0; break; }  // 0.2 s
+                }
+            }
+            if (__builtin_amdgcn_readfirstlane(ok)) {
+                const double *hr = q.hrec + ((size_t)q.prob * q.nc_max * CH + i) * HREC;
+                double hv[HREC];
+#pragma unroll
+                for (int e = 0; e < HREC; ++e) hv[e] = valid ? ld_sc1(hr + e) : -1.0;
+                const bool use = dirty && hv[6] == (double)off;
+                if (use) {
+                    double *dst = (sl ? rec2 : rec) + i;  // the slot the point uses from now on
+#pragma unroll
+                    for (int e = 0; e < 6; ++e) dst[(size_t)e * rs] = hv[e];
+                }
+                m &= ~__ballot(use);
+            }
+        }
         dbg_stamp(q.stamps, 0);
         const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
         const bool wlane = (lane & 3) == 0 && e6 < 6;
@@ -2069,6 +2104,73 @@ __device__ __forceinline__ void lm_update_wave(double tot, bool stamps) {
 }
 
 // ---------------------------------------------------------------------------
+// First-evaluation helper workgroup: for its problem's blocks hb, hb + H, ... every wave
+// projects the block at the initial pose and gathers the records of its eighth of the block's
+// supported points (gather_records: the main workgroup's own code, so the sums are the ones
+// it would form), then stores them with the texel offsets (write-through, drained) and, after
+// the workgroup's barrier, publishes each block with the launch's tag (MI355X_MICROARCH.md, sc1
+// hand-off).  No helper waits on anything.
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void helper_run(const LaunchArgs &a, int mmax) {
+    LMState &st = S();
+    const int h = (int)blockIdx.x - a.grid_main, p = h / a.helpers, hb = h % a.helpers;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    problem_begin(a.probs + p, p, mmax);
+    PC q = load_pc();
+    q.G = 1;
+    q.spec = 0;
+    q.helpers = q.hfirst = 0;
+    const double *X = lds_X(mmax);
+    double *rec = lds_rec(mmax);
+    const int rs = lds_rs(mmax);
+    double Re[9], te[3];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Re[k] = st.Re[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) te[k] = st.te[k];
+    double *out = a.hrec + (size_t)p * a.nc_max * CH * HREC;
+    const int nw = nwaves(), per = 64 / nw;
+    for (int blk = hb; blk * 64 < q.M; blk += a.helpers) {
+        const int i = blk * 64 + lane;
+        const bool valid = i < q.M;
+        int off = -1;
+        if (valid) {
+            double Pc[3];
+            transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
+            int x, y;
+            double qx, qy;
+            if (project_px(q.K, Pc, q.im_w, q.im_h, x, y, qx, qy)) {
+                const int row = (int)udiv((unsigned)y * (unsigned)q.Hf, q.dh);
+                const int col = (int)udiv((unsigned)x * (unsigned)q.Wf, q.dw);
+                off = row * q.Wf + col;
+            }
+        }
+        const bool mine = lane >= per * wave && lane < per * (wave + 1);
+        const unsigned long long m = __ballot(off >= 0 && mine);
+        const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
+        const bool wlane = (lane & 3) == 0 && e6 < 6;
+        const size_t fo = (size_t)(wlane ? e6 : 0) * rs + blk * 64;
+        const RecDst rd{rec + fo, rec + fo, 0ull};
+        if (m) gather_records<T, true, false>(q, m, off, 0, blk, rd, wlane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (valid && mine) {
+            double *o = out + (size_t)i * HREC;
+            for (int e = 0; e < 6; ++e) st_sc1(o + e, off >= 0 ? rec[(size_t)e * rs + i] : 0.0);
+            st_sc1(o + 6, (double)off);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (tid == 0) {
+        const int nb = (q.M + 63) / 64;
+        for (int blk = hb; blk < nb; blk += a.helpers)
+            __hip_atomic_store(reinterpret_cast<g_u64 *>(reinterpret_cast<uintptr_t>(a.hflag + (size_t)p * a.nc_max + blk)),
+                               a.htag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------
 // Specialised per launch (the launcher picks the variant): TEAM = G > 1, RATIO = the ratio
@@ -2084,7 +2186,8 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
     const int b = blockIdx.x, gw = a.gw;
     const int grp = b / (gw * G), rem = b % (gw * G);
     const int s = rem / gw;
-    const int team = grp * gw + rem % gw;
+    const bool helper = a.helpers > 0 && b >= a.grid_main;  // first-evaluation helper (helper_run)
+    const int team = helper ? 0 : grp * gw + rem % gw;
     if (team >= a.teams) return;
     const int tid = threadIdx.x;
     const int mmax = a.mmax;
@@ -2127,18 +2230,34 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
         for (int k = 0; k < NSTAMP; ++k) st.stamp_ph[tid >> 6][k] = 0;
         st.stamp_t[tid >> 6] = __builtin_amdgcn_s_memtime();
     }
+    constexpr bool kHelp = WPS == WPS_LATENCY && !TEAM && (VAR == VAR_GM_SPEC_H || VAR == VAR_NEAREST_SPEC_H);
+    if (helper) {
+        if constexpr (kHelp) helper_run<T>(a, mmax);
+        return;
+    }
     for (int p = team; p < a.n; p += a.teams) {
         problem_begin(a.probs + p, p, mmax);
         PC q = load_pc();
+        q.helpers = kHelp ? a.helpers : 0;
+        q.prob = p;
+        q.hrec = a.hrec;
+        q.hflag = a.hflag;
+        q.htag = a.htag;
+        bool first_eval = true;
         if constexpr (!TEAM) q.G = 1;
         q.use_ratio = RATIO ? 1 : 0;
         // speculation: the nearest-sampling variants of the latency build
-        constexpr bool kSpec = kSpecBuild && (VAR == VAR_GM_SPEC || VAR == VAR_NEAREST_SPEC) && WPS == WPS_LATENCY;
-        if constexpr (VAR == VAR_GM || VAR == VAR_F_GM || VAR == VAR_GM_SPEC) q.loss = FMPNP_GEMAN_MCCLURE;
+        constexpr bool kSpec = kSpecBuild && WPS == WPS_LATENCY &&
+                               (VAR == VAR_GM_SPEC || VAR == VAR_NEAREST_SPEC || VAR == VAR_GM_SPEC_H ||
+                                VAR == VAR_NEAREST_SPEC_H);
+        if constexpr (VAR == VAR_GM || VAR == VAR_F_GM || VAR == VAR_GM_SPEC || VAR == VAR_GM_SPEC_H)
+            q.loss = FMPNP_GEMAN_MCCLURE;
         q.bilinear = (VAR == VAR_BILINEAR || VAR == VAR_BIL_DIRECT) ? 1 : 0;
         long long ngath = 0;  // texel gathers of this wave for this problem
         while (!st.done) {
             if (ev_stamps && tid == 0 && p == team && st.n_evals < 63) ev_stamps[st.n_evals] = __builtin_amdgcn_s_memtime();
+            q.hfirst = first_eval && q.helpers > 0 && p == team;  // helpers serve each team's first problem
+            first_eval = false;
             // project, gather, loss (+ partials)
             // (double-buffered gathers in both builds; speculation in the latency build only)
             // (bilinear: the cell memo; VAR_BIL_DIRECT samples every point at every evaluation)
@@ -2146,7 +2265,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
             if constexpr (VAR == VAR_BILINEAR)
                 lmax = eval_pass_bil<T>(q, mmax, ngath);
             else
-                lmax = eval_pass<T, true, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST), kSpec>(q, mmax, ngath);
+                lmax = eval_pass<T, true, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST), kSpec, kHelp>(q, mmax, ngath);
             if (q.use_ratio) {
                 if (!ratio_exchange(lmax)) break;
                 contrib_pass(q, mmax);

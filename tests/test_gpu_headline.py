@@ -173,3 +173,28 @@ def test_speculation_settings_change_nothing(w0, cap, monkeypatch):
     np.testing.assert_array_equal(tb["cost"], t["cost"])
     np.testing.assert_array_equal(tb["n_supported"], t["n_supported"])
     np.testing.assert_array_equal(tb["lam"], t["lam"])
+
+
+@pytest.mark.parametrize("B,init,ratio", [(1, "easy", None), (1, "hard", 0.8), (4, "hard", None), (16, "easy", None)])
+def test_first_evaluation_helpers_change_nothing(B, init, ratio, monkeypatch):
+    """Small batches: helper workgroups gather the first evaluation's records of each problem's
+    64-point blocks on otherwise idle CUs (fmpnp_lm_impl.h helper_run).  Same gather code at the
+    same pose, so poses, costs, support counts, the LM schedule and the gather counts are
+    bit-identical to the run without helpers."""
+    probs = [packed_problem(synth.problem_inputs(512, 256, 240, 320, seed=40 + q, device=DEV, init=init), "fgrad")
+             for q in range(B)]
+    o = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, ratio_threshold=ratio, dtype=_lib.F32)
+    monkeypatch.setenv("FMPNP_HELPERS", "0")
+    base, tb = rf.refine(probs, o, trace=True)
+    assert _lib.last_launch()["grid"] == B
+    monkeypatch.setenv("FMPNP_HELPERS", "1")
+    res, tr = rf.refine(probs, o, trace=True)
+    assert _lib.last_launch()["grid"] > B  # the helpers ran
+    for q in range(B):
+        a, r = base[q], res[q]
+        assert np.array_equal(a["R"], r["R"]) and np.array_equal(a["t"], r["t"]), q
+        assert a["best_cost"] == r["best_cost"] and a["n_evals"] == r["n_evals"] and a["status"] == r["status"]
+        assert a["texel_gathers"] == r["texel_gathers"]
+        np.testing.assert_array_equal(tb[q]["cost"], tr[q]["cost"])
+        np.testing.assert_array_equal(tb[q]["n_supported"], tr[q]["n_supported"])
+        np.testing.assert_array_equal(tb[q]["lam"], tr[q]["lam"])
