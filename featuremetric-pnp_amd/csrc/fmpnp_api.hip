@@ -200,9 +200,11 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
         const bool on = !eh || atoi(eh) != 0;
         // (helpers beside the padded main grid, all resident at once: the mains wait on them)
         const long spare = ((long)ncu - P.grid) / std::max(n, 1);
-        // (the speculating variants carry the hand-off; a single helper per problem -- B > CUs/3 --
-        // measured slower at B = 128: 0.380 vs 0.360 ms, the first evaluation being HBM-bound there)
-        if (on && P.spec && G == 1 && P.wps == WPS_LATENCY && P.teams == n && P.nc_max >= 2 && spare >= 2)
+        // (packed nearest memoised forward runs; a single helper per problem -- B > CUs/3 -- measured
+        // slower at B = 128: 0.380 vs 0.360 ms, the first evaluation being HBM-bound there)
+        if (on && G == 1 && P.wps == WPS_LATENCY && !bil_memo && opt->sampling == FMPNP_NEAREST &&
+            opt->no_memo != 1 && opt->mode == FMPNP_MODE_FORWARD && opt->layout == FMPNP_LAYOUT_FGRAD &&
+            P.teams == n && P.nc_max >= 2 && spare >= 2)
             P.helpers = (int)std::min<long>(std::min<long>(spare, P.nc_max), 8);
     }
     P.grid = P.grid_main + n * P.helpers;

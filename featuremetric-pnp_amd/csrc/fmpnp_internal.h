@@ -95,9 +95,10 @@ inline int spec_variant(int var) {
 }
 // ... and those two with the first-evaluation helpers' hand-off compiled in (small batches:
 // LaunchArgs::helpers; the headline-size batches run without it and without its code)
-constexpr int VAR_GM_SPEC_H = 8, VAR_NEAREST_SPEC_H = 9;
+constexpr int VAR_GM_SPEC_H = 8, VAR_NEAREST_SPEC_H = 9, VAR_GM_H = 10, VAR_NEAREST_H = 11;
 inline int help_variant(int var) {
-    return var == VAR_GM_SPEC ? VAR_GM_SPEC_H : var == VAR_NEAREST_SPEC ? VAR_NEAREST_SPEC_H : var;
+    return var == VAR_GM_SPEC ? VAR_GM_SPEC_H : var == VAR_NEAREST_SPEC ? VAR_NEAREST_SPEC_H
+         : var == VAR_GM ? VAR_GM_H : var == VAR_NEAREST ? VAR_NEAREST_H : var;
 }
 int lm_variant(const fmpnp_options &o);
 const void *lm_kernel_ptr(int dtype, int wps, bool team, bool ratio, int var);

@@ -17,6 +17,13 @@ static LmFn pick_var(int var) {
         }
         return nullptr;
     }
+    if (var == VAR_GM_H || var == VAR_NEAREST_H) {  // first-evaluation helpers without speculation
+        if constexpr (WPS == WPS_LATENCY && !TEAM) {
+            if (var == VAR_GM_H) return lm_kernel<float, WPS, TEAM, RATIO, VAR_GM_H>;
+            return lm_kernel<float, WPS, TEAM, RATIO, VAR_NEAREST_H>;
+        }
+        return nullptr;
+    }
     if (var == VAR_BILINEAR) return nullptr;  // the cell memo runs on the WPS_WIDE build only
     if (var == VAR_BIL_DIRECT) return lm_kernel<float, WPS, TEAM, RATIO, VAR_BIL_DIRECT>;
     if constexpr (WPS == WPS_LATENCY) {  // FMPNP_LAYOUT_F (the planner keeps it on the latency build)

@@ -2230,7 +2230,8 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
         for (int k = 0; k < NSTAMP; ++k) st.stamp_ph[tid >> 6][k] = 0;
         st.stamp_t[tid >> 6] = __builtin_amdgcn_s_memtime();
     }
-    constexpr bool kHelp = WPS == WPS_LATENCY && !TEAM && (VAR == VAR_GM_SPEC_H || VAR == VAR_NEAREST_SPEC_H);
+    constexpr bool kHelp = WPS == WPS_LATENCY && !TEAM && (VAR == VAR_GM_SPEC_H || VAR == VAR_NEAREST_SPEC_H ||
+                                                           VAR == VAR_GM_H || VAR == VAR_NEAREST_H);
     if (helper) {
         if constexpr (kHelp) helper_run<T>(a, mmax);
         return;
@@ -2250,7 +2251,8 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
         constexpr bool kSpec = kSpecBuild && WPS == WPS_LATENCY &&
                                (VAR == VAR_GM_SPEC || VAR == VAR_NEAREST_SPEC || VAR == VAR_GM_SPEC_H ||
                                 VAR == VAR_NEAREST_SPEC_H);
-        if constexpr (VAR == VAR_GM || VAR == VAR_F_GM || VAR == VAR_GM_SPEC || VAR == VAR_GM_SPEC_H)
+        if constexpr (VAR == VAR_GM || VAR == VAR_F_GM || VAR == VAR_GM_SPEC || VAR == VAR_GM_SPEC_H ||
+                      VAR == VAR_GM_H)
             q.loss = FMPNP_GEMAN_MCCLURE;
         q.bilinear = (VAR == VAR_BILINEAR || VAR == VAR_BIL_DIRECT) ? 1 : 0;
         long long ngath = 0;  // texel gathers of this wave for this problem

@@ -175,15 +175,18 @@ def test_speculation_settings_change_nothing(w0, cap, monkeypatch):
     np.testing.assert_array_equal(tb["lam"], t["lam"])
 
 
-@pytest.mark.parametrize("B,init,ratio", [(1, "easy", None), (1, "hard", 0.8), (4, "hard", None), (16, "easy", None)])
-def test_first_evaluation_helpers_change_nothing(B, init, ratio, monkeypatch):
+@pytest.mark.parametrize("B,init,ratio,C,spec", [(1, "easy", None, 256, True), (1, "hard", 0.8, 256, True),
+                                                  (4, "hard", None, 256, True), (16, "easy", None, 256, True),
+                                                  (2, "hard", None, 512, True), (1, "easy", None, 256, False)])
+def test_first_evaluation_helpers_change_nothing(B, init, ratio, C, spec, monkeypatch):
     """Small batches: helper workgroups gather the first evaluation's records of each problem's
     64-point blocks on otherwise idle CUs (fmpnp_lm_impl.h helper_run).  Same gather code at the
     same pose, so poses, costs, support counts, the LM schedule and the gather counts are
     bit-identical to the run without helpers."""
-    probs = [packed_problem(synth.problem_inputs(512, 256, 240, 320, seed=40 + q, device=DEV, init=init), "fgrad")
+    H, W = (240, 320) if C == 256 else (120, 160)
+    probs = [packed_problem(synth.problem_inputs(512, C, H, W, seed=40 + q, device=DEV, init=init), "fgrad")
              for q in range(B)]
-    o = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, ratio_threshold=ratio, dtype=_lib.F32)
+    o = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, ratio_threshold=ratio, dtype=_lib.F32, speculate=spec)
     monkeypatch.setenv("FMPNP_HELPERS", "0")
     base, tb = rf.refine(probs, o, trace=True)
     assert _lib.last_launch()["grid"] == B
