@@ -201,3 +201,22 @@ def test_first_evaluation_helpers_change_nothing(B, init, ratio, C, spec, monkey
         np.testing.assert_array_equal(tb[q]["cost"], tr[q]["cost"])
         np.testing.assert_array_equal(tb[q]["n_supported"], tr[q]["n_supported"])
         np.testing.assert_array_equal(tb[q]["lam"], tr[q]["lam"])
+
+
+def test_first_evaluation_helpers_fp64_storage(monkeypatch):
+    """The helpers' hand-off with fp64 texels (VAR_GM_H, the non-speculating variant at C = 256
+    fp64): bit-identical to the run without helpers."""
+    inp = synth.problem_inputs(512, 256, 240, 320, seed=47, device=DEV, init="hard")
+    feats = rf.pack_features(inp["fmap"].double(), storage=torch.float64, device=DEV)
+    prob = rf.make_problem(feats, inp["fref"].double(), inp["pts3d"], inp["K"], inp["im_width"], inp["im_height"],
+                           inp["R0"], inp["t0"])
+    o = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F64)
+    monkeypatch.setenv("FMPNP_HELPERS", "0")
+    (base,), (tb,) = rf.refine([prob], o, trace=True)
+    monkeypatch.setenv("FMPNP_HELPERS", "1")
+    (res,), (tr,) = rf.refine([prob], o, trace=True)
+    assert _lib.last_launch()["grid"] > 1
+    assert np.array_equal(base["R"], res["R"]) and np.array_equal(base["t"], res["t"])
+    assert base["best_cost"] == res["best_cost"] and base["texel_gathers"] == res["texel_gathers"]
+    np.testing.assert_array_equal(tb["cost"], tr["cost"])
+    np.testing.assert_array_equal(tb["n_supported"], tr["n_supported"])
