@@ -202,12 +202,15 @@ int fmpnp_gather_reference_batch(int n, const void *const *ref_chw, const int *r
 int fmpnp_point_costs(const fmpnp_problem *prob, int layout, int dtype, double *cost, int *supported,
                       void *hip_stream);
 
-/* Device workspace needed by fmpnp_refine_batch_async for n problems. */
+/* Device workspace needed by fmpnp_refine_batch_async for n problems (team exchange slots and,
+ * for small batches, the first-evaluation helpers' records; no initialisation needed, reusable
+ * by later launches on the same stream). */
 size_t fmpnp_workspace_size(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt);
 
 /* Asynchronous batched refinement: descriptors, results and trace in DEVICE
- * memory; nothing is synchronised.  probs_host (may be NULL) is only read to
- * size the launch; when NULL, max_N must bound every problem's N. */
+ * memory; nothing is synchronised.  probs_host: the same descriptors in host memory
+ * (required: the launch plan reads every problem's sizes and channel slice); max_N is
+ * unused (kept for ABI stability). */
 int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem *probs_host, int n, int max_N,
                              const fmpnp_options *opt, fmpnp_result *results_dev, fmpnp_trace_entry *trace_dev,
                              int trace_stride, void *workspace, size_t workspace_bytes, void *hip_stream);
