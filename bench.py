@@ -32,7 +32,9 @@ restatement at 1 thread and at every core of the job's share) on a bounded sampl
 poses are compared with the GPU's for the same queries.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-       N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+       N > 1 outside a launcher: bench.py starts N rank processes itself (torch.distributed.run,
+       127.0.0.1, a free port) before anything touches the GPU and exits with their status;
+       rank 0 prints the line.  Under a launcher (WORLD_SIZE set) --gpus must equal WORLD_SIZE.
 """
 import argparse
 import json
@@ -83,6 +85,24 @@ def parse():
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without a launcher: run N ranks under torch.distributed.run
+    (one process per GPU) as a CHILD process -- this process has not touched the GPU and never
+    execs -- and return its exit status.  Rank 0's JSON line reaches stdout directly."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] --gpus {n}: launching {n} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
 def workload_tag(B, init, ratio, memo, sampling, layout, spec=True):
@@ -146,7 +166,18 @@ def roofline(tag, res, kernel_s, B, sampling, layout):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))  # before any torch.cuda / HIP call
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"[bench] error: --gpus {args.gpus} but the launcher started {world} ranks (WORLD_SIZE)")
+        sys.exit(2)
+    if os.environ.get("FMPNP_BENCH_DRYRUN"):  # CPU test of the launch path: report the rank, touch no GPU
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": world,
+                          "queries": list(__import__("fmpnp.shard", fromlist=["x"]).query_indices(
+                              int(os.environ.get("RANK", "0")), world, per_rank=args.batch,
+                              global_batch=args.global_batch))}), flush=True)
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
@@ -218,7 +249,9 @@ def main():
     statuses = sorted({r["status"] for r in res})
     if any(s & _lib.STATUS_SYNC_TIMEOUT for s in statuses):
         raise RuntimeError("sync timeout in the LM kernel")
-    value = B * world * args.steps / elapsed
+    # every rank's queries: the fixed total (strong scaling), else the per-rank batch on each rank
+    total = args.global_batch if args.global_batch > 0 else args.batch * world
+    value = total * args.steps / elapsed
     tag = workload_tag(B, args.init, args.ratio, memo, args.sampling, args.layout, not args.no_spec)
 
     extras = {}
@@ -248,8 +281,10 @@ def main():
                        "init": args.init, "ratio_threshold": args.ratio, "memoised": memo,
                        "speculative_gathers": memo and not args.no_spec and _lib.spec_build(),
                        "sampling": args.sampling, "layout": args.layout,
-                       "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": f"query sharding x{world} (no collectives)", "launch": launch},
+                       "batch_per_gpu": B, "global_batch": total,
+                       "parallelism": f"query sharding x{world} (no collectives)", "launch": launch,
+                       "ranks": world, "devices_visible": ndev,
+                       "backend": (backend if dist else None)},
             "gn_iters_per_s": round(value * ITERS, 1),
             "roofline": roofline(tag, res, kernel_s, B, args.sampling, args.layout),
             "kernel_timing": f"HIP events on the launch stream around every {every}-th of the {args.steps} timed "

@@ -24,6 +24,7 @@ namespace {
 struct Plan {
     int G = 1, teams = 1, teams_pad = 8, gw = 8, grid = 8, nc_max = 1, max_n = 0;
     int mmax = 0, lds = 0, wps = WPS_LATENCY, spec = 0, helpers = 0, grid_main = 8;
+    int var = 0, ratio = 0, dtype = 0;  // the kernel variant the launch runs
     size_t ws_counters = 0, ws_partials = 0, ws_max = 0, ws_hrec = 0, ws_hflag = 0, ws_total = 0;
 };
 
@@ -196,8 +197,10 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     // B = 32 0.310 / 0.302, B = 64 0.341 / 0.333); FMPNP_HELPERS=0 switches them off
     P.grid_main = P.grid;
     {
+        // opt->helpers < 0 switches them off (callers sharing the device with other kernels),
+        // > 0 caps them; FMPNP_HELPERS=0 (environment) switches them off too
         const char *eh = getenv("FMPNP_HELPERS");
-        const bool on = !eh || atoi(eh) != 0;
+        const bool on = (!eh || atoi(eh) != 0) && opt->helpers >= 0;
         // (helpers beside the padded main grid, all resident at once: the mains wait on them)
         const long spare = ((long)ncu - P.grid) / std::max(n, 1);
         // (packed nearest memoised forward runs; a single helper per problem -- B > CUs/3 -- measured
@@ -205,12 +208,17 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
         if (on && G == 1 && P.wps == WPS_LATENCY && !bil_memo && opt->sampling == FMPNP_NEAREST &&
             opt->no_memo != 1 && opt->mode == FMPNP_MODE_FORWARD && opt->layout == FMPNP_LAYOUT_FGRAD &&
             P.teams == n && P.nc_max >= 2 && spare >= 2)
-            P.helpers = (int)std::min<long>(std::min<long>(spare, P.nc_max), 8);
+            P.helpers = (int)std::min<long>(std::min<long>(std::min<long>(spare, P.nc_max), 8),
+                                            opt->helpers > 0 ? opt->helpers : 8);
     }
     P.grid = P.grid_main + n * P.helpers;
     P.ws_hrec = P.helpers ? align_up((size_t)n * P.nc_max * CH * HREC * sizeof(double), 256) : 0;
     P.ws_hflag = P.helpers ? align_up((size_t)n * P.nc_max * sizeof(unsigned long long), 256) : 0;
     P.ws_total = P.ws_counters + P.ws_partials + P.ws_max + P.ws_hrec + P.ws_hflag;
+    P.var = P.spec ? spec_variant(lm_variant(*opt)) : lm_variant(*opt);
+    if (P.helpers) P.var = help_variant(P.var);
+    P.ratio = opt->use_ratio != 0;
+    P.dtype = opt->dtype;
     *pl = P;
     return 0;
 }
@@ -416,8 +424,8 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
         a.spec_w0 = ew ? std::max(0, atoi(ew)) : 4;
     }
     {
-        static const int dbg = [] { const char *e = getenv("FMPNP_DBG"); return e ? atoi(e) : 0; }();
-        a.dbg = dbg;
+        const char *e = getenv("FMPNP_DBG");  // debug knob, read per launch (fmpnp_internal.h LaunchArgs::dbg)
+        a.dbg = e ? atoi(e) : 0;
     }
     // teams of G > 1 workgroups count their arrivals and add their texel gathers into zeroed
     // memory; with G = 1 the kernel writes every result field itself and nothing is zeroed
@@ -428,7 +436,7 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
         e = hipMemsetAsync(results_dev, 0, sizeof(fmpnp_result) * (size_t)n, s);  // texel_gathers accumulate
         if (e != hipSuccess) return (int)e;
     }
-    e = launch_lm(a, opt->dtype, P.grid, (size_t)P.lds, s);
+    e = launch_lm(a, opt->dtype, P.var, P.grid, (size_t)P.lds, s);
     g_last = P;
     return (int)e;
 }
@@ -499,6 +507,35 @@ int fmpnp_last_launch(int *teams, int *wgs_per_problem, int *grid, int *lds_byte
     if (wgs_per_problem) *wgs_per_problem = g_last.G;
     if (grid) *grid = g_last.grid;
     if (lds_bytes) *lds_bytes = g_last.lds;
+    return 0;
+}
+
+static void plan_info(const Plan &P, fmpnp_launch_info *o) {
+    o->teams = P.teams;
+    o->wgs_per_problem = P.G;
+    o->grid = P.grid;
+    o->lds_bytes = P.lds;
+    o->build = P.wps;
+    o->variant = P.var;
+    o->team = P.G > 1;
+    o->ratio = P.ratio;
+    o->dtype = P.dtype;
+    o->helpers = P.helpers;
+    o->speculate = P.spec;
+}
+
+int fmpnp_plan(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt, fmpnp_launch_info *out) {
+    if (!out || n <= 0 || !probs_host) return FMPNP_EINVAL;
+    Plan P;
+    const int rc = make_plan(probs_host, n, opt, &P);
+    if (rc) return rc;
+    plan_info(P, out);
+    return 0;
+}
+
+int fmpnp_last_launch_info(fmpnp_launch_info *out) {
+    if (!out) return FMPNP_EINVAL;
+    plan_info(g_last, out);
     return 0;
 }
 

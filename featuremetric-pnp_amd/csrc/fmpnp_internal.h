@@ -27,11 +27,11 @@ constexpr int MAX_G = 64;       // workgroups per problem
 // WPS_THROUGHPUT = 256-thread workgroups (4 waves, two 64-point blocks per wave at N=512),
 // two resident per CU, so one problem's serial LM tail overlaps the other's point work
 // (batches of >= 2 problems per CU).  Both keep 2 waves per SIMD: up to 256 VGPRs.
-constexpr int WPS_LATENCY = 2, WPS_THROUGHPUT = 4;
+constexpr int WPS_LATENCY = FMPNP_BUILD_LATENCY, WPS_THROUGHPUT = FMPNP_BUILD_THROUGHPUT;
 constexpr int NT_THROUGHPUT = 256;
 // WPS_WIDE = 256-thread workgroups, one wave per SIMD: up to 512 registers per lane (VGPRs +
 // AGPRs), for the bilinear cell memo (its LDS allows one workgroup per CU anyway)
-constexpr int WPS_WIDE = 1;
+constexpr int WPS_WIDE = FMPNP_BUILD_WIDE;
 
 // Kernel arguments (by value).
 struct LaunchArgs {
@@ -51,7 +51,8 @@ struct LaunchArgs {
     int spec;                     // speculative next-texel gathers (memoised nearest modes)
     int spec_cap;                 // at most this many speculative gathers per wave per evaluation
     int spec_w0;                  // waves >= spec_w0 speculate (the later wave of each SIMD: 4)
-    int dbg;                      // debug knob (FMPNP_DBG): bit 0 census only, bit 1 no consume
+    int dbg;                      // debug knob (FMPNP_DBG): bit 2 per-evaluation stamps, bit 3 helpers
+                                  // never publish (exercises the main workgroups' bounded wait)
     // first-evaluation helpers (small batches, one workgroup per problem): workgroups
     // grid_main .. grid_main + n * helpers - 1 gather the initial pose's records of their
     // problem's blocks into hrec and publish each block with a tagged flag (lm_kernel)
@@ -79,23 +80,26 @@ constexpr int BIL_NB = 54;
 constexpr int BIL_MAX_M = 256;
 size_t lm_dyn_lds_bytes(int mmax, int nc_max, bool spec, bool bil_memo = false);
 
-hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream);
+// var: the plan's variant (spec_variant / help_variant already applied)
+hipError_t launch_lm(const LaunchArgs &a, int dtype, int var, int grid, size_t lds, hipStream_t stream);
 // LM kernel variants (fmpnp_lm_impl.h): Geman-McClure forward with nearest sampling (the
 // hot path), any loss / mode with nearest sampling, bilinear sampling
-constexpr int VAR_NEAREST = 0, VAR_GM = 1, VAR_BILINEAR = 2;
+// (the values are the public FMPNP_VAR_* codes of fmpnp_launch_info)
+constexpr int VAR_NEAREST = FMPNP_VAR_NEAREST, VAR_GM = FMPNP_VAR_GM, VAR_BILINEAR = FMPNP_VAR_BILINEAR;
 // ... and the same two nearest variants on FMPNP_LAYOUT_F maps (fp32 only); bilinear sampling
 // without the cell memo (no_memo = 1: every supported point sampled at every evaluation)
-constexpr int VAR_F_NEAREST = 3, VAR_F_GM = 4, VAR_BIL_DIRECT = 5;
+constexpr int VAR_F_NEAREST = FMPNP_VAR_F_NEAREST, VAR_F_GM = FMPNP_VAR_F_GM, VAR_BIL_DIRECT = FMPNP_VAR_BIL_DIRECT;
 // ... and the two packed nearest variants with the speculative next-texel gathers compiled in
 // (the latency build, one workgroup per problem: the planner's P.spec); the other variants are
 // built without them, so their code does not pay for speculation they do not run
-constexpr int VAR_GM_SPEC = 6, VAR_NEAREST_SPEC = 7;
+constexpr int VAR_GM_SPEC = FMPNP_VAR_GM_SPEC, VAR_NEAREST_SPEC = FMPNP_VAR_NEAREST_SPEC;
 inline int spec_variant(int var) {
     return var == VAR_GM ? VAR_GM_SPEC : var == VAR_NEAREST ? VAR_NEAREST_SPEC : var;
 }
 // ... and those two with the first-evaluation helpers' hand-off compiled in (small batches:
 // LaunchArgs::helpers; the headline-size batches run without it and without its code)
-constexpr int VAR_GM_SPEC_H = 8, VAR_NEAREST_SPEC_H = 9, VAR_GM_H = 10, VAR_NEAREST_H = 11;
+constexpr int VAR_GM_SPEC_H = FMPNP_VAR_GM_SPEC_H, VAR_NEAREST_SPEC_H = FMPNP_VAR_NEAREST_SPEC_H,
+              VAR_GM_H = FMPNP_VAR_GM_H, VAR_NEAREST_H = FMPNP_VAR_NEAREST_H;
 inline int help_variant(int var) {
     return var == VAR_GM_SPEC ? VAR_GM_SPEC_H : var == VAR_NEAREST_SPEC ? VAR_NEAREST_SPEC_H
          : var == VAR_GM ? VAR_GM_H : var == VAR_NEAREST ? VAR_NEAREST_H : var;

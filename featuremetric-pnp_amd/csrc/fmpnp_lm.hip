@@ -56,10 +56,8 @@ int lm_variant(const fmpnp_options &o) {
     return gm ? VAR_GM : VAR_NEAREST;
 }
 
-hipError_t launch_lm(const LaunchArgs &a, int dtype, int grid, size_t lds, hipStream_t stream) {
+hipError_t launch_lm(const LaunchArgs &a, int dtype, int var, int grid, size_t lds, hipStream_t stream) {
     typedef void (*LmFn)(LaunchArgs);
-    int var = a.spec ? spec_variant(lm_variant(a.opt)) : lm_variant(a.opt);
-    if (a.helpers) var = help_variant(var);
     const LmFn f = (LmFn)lm_kernel_ptr(dtype, a.wps, a.G > 1, a.opt.use_ratio != 0, var);
     if (!f) return hipErrorInvalidDeviceFunction;
     hipLaunchKernelGGL(f, dim3(grid), dim3(a.wps == WPS_LATENCY ? NT : NT_THROUGHPUT), lds, stream, a);

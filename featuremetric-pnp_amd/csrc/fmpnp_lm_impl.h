@@ -1611,6 +1611,12 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
             // helper workgroup (the same gather code at the same pose: identical sums); a point
             // whose texel the helper saw differently, or a helper that never publishes, is
             // gathered here as usual
+            // Hand-off (MI355X_MICROARCH.md, Workgroup dispatch: producer release + flag, consumer
+            // relaxed poll + ONE agent-scope acquire): the helper stored its records, drained,
+            // released (buffer_wbl2) and then stored this launch's tag; lane 0 polls the tag, and
+            // after the match the wave acquires before any lane reads a record, so no read can see
+            // bytes older than the tag -- in particular not an earlier launch's records left in a
+            // reused workspace (the tag is launch-unique, the texel offset is checked as well).
             const unsigned long long *flag = q.hflag + (size_t)q.prob * q.nc_max + blk;
             int ok = 1;
             if (lane == 0) {
@@ -1620,8 +1626,12 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
                     __builtin_amdgcn_s_sleep(1);
                     if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) { ok = 0; break; }  // 0.2 s
                 }
+                // a helper that never published (kept from being resident by other kernels): the
+                // block is gathered here as usual; reported, results unaffected
+                if (!ok) atomicOr(&st.status, FMPNP_STATUS_HELPER_WAIT);
             }
             if (__builtin_amdgcn_readfirstlane(ok)) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every lane: no record read above the poll
                 const double *hr = q.hrec + ((size_t)q.prob * q.nc_max * CH + i) * HREC;
                 double hv[HREC];
 #pragma unroll
@@ -2162,7 +2172,11 @@ __device__ __forceinline__ void helper_run(const LaunchArgs &a, int mmax) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
-    if (tid == 0) {
+    if (tid == 0 && !(a.dbg & 8)) {  // (debug bit 3: never publish -- the mains' bounded wait)
+        // release the records before the tags (the explicit wait: the compiler may drop the one
+        // after buffer_wbl2, MI355X_MICROARCH.md "Compiler hazard")
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int nb = (q.M + 63) / 64;
         for (int blk = hb; blk < nb; blk += a.helpers)
             __hip_atomic_store(reinterpret_cast<g_u64 *>(reinterpret_cast<uintptr_t>(a.hflag + (size_t)p * a.nc_max + blk)),

@@ -20,6 +20,13 @@ LAYOUT_FGRAD, LAYOUT_F = 0, 1
 F32, F64 = 0, 1
 MODE_FORWARD, MODE_COMPUTE_COST = 0, 1
 STATUS_OK, STATUS_NO_SUPPORT, STATUS_NAN, STATUS_NO_SUPPORT_TRIAL, STATUS_SYNC_TIMEOUT = 0, 1, 2, 4, 8
+STATUS_HELPER_WAIT = 16  # informational: a first-evaluation helper did not publish in time (results unaffected)
+ABI_VERSION = 2
+# LM kernel builds and variants (fmpnp_launch_info)
+BUILD_WIDE, BUILD_LATENCY, BUILD_THROUGHPUT = 1, 2, 4
+BUILD_NAMES = {BUILD_WIDE: "wide", BUILD_LATENCY: "latency", BUILD_THROUGHPUT: "throughput"}
+VARIANT_NAMES = ["NEAREST", "GM", "BILINEAR", "F_NEAREST", "F_GM", "BIL_DIRECT", "GM_SPEC", "NEAREST_SPEC",
+                 "GM_SPEC_H", "NEAREST_SPEC_H", "GM_H", "NEAREST_H"]
 ERRORS = {-1: "EINVAL", -2: "EALIGN", -3: "ENOMEM", -4: "ETOOBIG", -5: "ENODEV"}
 
 
@@ -28,7 +35,7 @@ class Options(ctypes.Structure):
                 ("use_ratio", ctypes.c_int), ("ratio_threshold", ctypes.c_double), ("loss", ctypes.c_int),
                 ("barron_alpha", ctypes.c_double), ("sampling", ctypes.c_int), ("dtype", ctypes.c_int),
                 ("wgs_per_problem", ctypes.c_int), ("max_teams", ctypes.c_int), ("no_memo", ctypes.c_int),
-                ("layout", ctypes.c_int), ("sobel_flags", ctypes.c_int)]
+                ("layout", ctypes.c_int), ("sobel_flags", ctypes.c_int), ("helpers", ctypes.c_int)]
 
 
 class Problem(ctypes.Structure):
@@ -53,10 +60,17 @@ class TraceEntry(ctypes.Structure):
                 ("n_kept", ctypes.c_int), ("accepted", ctypes.c_int)]
 
 
+class LaunchInfo(ctypes.Structure):
+    _fields_ = [("teams", ctypes.c_int), ("wgs_per_problem", ctypes.c_int), ("grid", ctypes.c_int),
+                ("lds_bytes", ctypes.c_int), ("build", ctypes.c_int), ("variant", ctypes.c_int),
+                ("team", ctypes.c_int), ("ratio", ctypes.c_int), ("dtype", ctypes.c_int), ("helpers", ctypes.c_int),
+                ("speculate", ctypes.c_int)]
+
+
 EXPORTS = ["fmpnp_abi_version", "fmpnp_build_info", "fmpnp_device_check", "fmpnp_pack_features",
            "fmpnp_gather_reference", "fmpnp_gather_reference_async", "fmpnp_pack_features_batch", "fmpnp_pack_features_f",
            "fmpnp_gather_reference_batch", "fmpnp_workspace_size", "fmpnp_refine_batch_async", "fmpnp_refine_batch",
-           "fmpnp_last_launch", "fmpnp_debug_stamps"]
+           "fmpnp_last_launch", "fmpnp_debug_stamps", "fmpnp_plan", "fmpnp_last_launch_info"]
 
 _LIB = None
 
@@ -103,7 +117,11 @@ def load():
     L.fmpnp_refine_batch.restype = i
     L.fmpnp_last_launch.argtypes = [ctypes.POINTER(i)] * 4
     L.fmpnp_last_launch.restype = i
-    if L.fmpnp_abi_version() != 1:
+    L.fmpnp_plan.argtypes = [ctypes.POINTER(Problem), i, ctypes.POINTER(Options), ctypes.POINTER(LaunchInfo)]
+    L.fmpnp_plan.restype = i
+    L.fmpnp_last_launch_info.argtypes = [ctypes.POINTER(LaunchInfo)]
+    L.fmpnp_last_launch_info.restype = i
+    if L.fmpnp_abi_version() != ABI_VERSION:
         raise FmpnpError("libfmpnp ABI mismatch")
     _LIB = L
     return L
@@ -137,11 +155,29 @@ def stream_ptr(device=None):
 
 
 def spec_build():
-    """True when libfmpnp.so was built with the speculative next-texel gathers (-DFMPNP_SPEC=1)."""
+    """True when libfmpnp.so has the speculative next-texel gathers compiled in (the default;
+    a -DFMPNP_SPEC=0 build leaves them out).  Per launch, fmpnp_options.no_memo = 2 turns them off."""
     return b"speculative_gathers=1" in load().fmpnp_build_info()
 
 
+def _info_dict(info):
+    d = {name: getattr(info, name) for name, _ in LaunchInfo._fields_}
+    d["build_name"] = BUILD_NAMES.get(info.build, str(info.build))
+    d["variant_name"] = VARIANT_NAMES[info.variant] if 0 <= info.variant < len(VARIANT_NAMES) else str(info.variant)
+    d["dtype_name"] = "f64" if info.dtype == F64 else "f32"
+    return d
+
+
 def last_launch():
-    v = [ctypes.c_int() for _ in range(4)]
-    load().fmpnp_last_launch(*[ctypes.byref(x) for x in v])
-    return dict(teams=v[0].value, wgs_per_problem=v[1].value, grid=v[2].value, lds_bytes=v[3].value)
+    """Plan of this thread's last LM launch: geometry, build, kernel variant, helpers."""
+    info = LaunchInfo()
+    load().fmpnp_last_launch_info(ctypes.byref(info))
+    return _info_dict(info)
+
+
+def plan(descs, n, options):
+    """The launch plan (as last_launch()) for n fmpnp_problem descriptors and options, without
+    launching (needs the device)."""
+    info = LaunchInfo()
+    check(load().fmpnp_plan(descs, n, ctypes.byref(options), ctypes.byref(info)), "fmpnp_plan")
+    return _info_dict(info)

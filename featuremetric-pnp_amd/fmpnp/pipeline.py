@@ -52,12 +52,13 @@ class RefinePipeline:
         kw = config.model_kwargs()
         kw.update(model_kwargs or {})
         loss_code, alpha = _losses.resolve(kw["loss_fn"])
-        # one workgroup per query by default: the LM launch then leaves the other CUs to the next
-        # batch's pack and gather on the prep stream, and no workgroup of a launch ever waits on
-        # another that a concurrent kernel could keep from being resident
+        # one workgroup per query by default, and no first-evaluation helpers: the LM launch then
+        # leaves the other CUs to the next batch's pack and gather on the prep stream, and no
+        # workgroup of a launch waits on another one (a helper) that those concurrent kernels
+        # could keep from being resident
         self.options = _rf.make_options(kw["n_iters"], kw["lambda_"], loss_code, alpha, kw.get("ratio_threshold"),
                                         _rf._dtype_code(storage), sampling=sampling,
-                                        wgs_per_problem=int(wgs_per_problem))
+                                        wgs_per_problem=int(wgs_per_problem), helpers=-1)
         self.sampling = sampling
         self.depth = max(1, int(depth))
         # "f" (f plane only, gradients formed in the LM gather) wherever it applies: fp32

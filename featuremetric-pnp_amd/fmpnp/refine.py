@@ -255,12 +255,13 @@ def bind_layout(problems, options):
 
 def make_options(n_iters, lambda0=0.01, loss=_lib.SQUARED, barron_alpha=0.0, ratio_threshold=None,
                  dtype=_lib.F32, mode=_lib.MODE_FORWARD, wgs_per_problem=0, max_teams=0, memoize=True,
-                 sampling="nearest", speculate=True):
+                 sampling="nearest", speculate=True, helpers=0):
     """fmpnp_options.  sampling: "nearest" (the reference's indexing_, model.py:74-97) or
     "bilinear" (extension: 2x2 taps of f, gx, gy; definition in fmpnp_device.h bilinear_taps,
     checked against the oracle's restatement -- no reference counterpart, parity unpinned).
     memoize: re-gather a point's texel only when it changed; speculate (memoised nearest
-    forward runs): gather the predicted next texels beside the LM tail.  Neither changes
+    forward runs): gather the predicted next texels beside the LM tail; helpers: first-evaluation
+    helper workgroups per problem (0 = planner, < 0 = none, > 0 = cap).  None of them changes
     the results."""
     o = _lib.Options()
     o.mode = int(mode)
@@ -275,6 +276,7 @@ def make_options(n_iters, lambda0=0.01, loss=_lib.SQUARED, barron_alpha=0.0, rat
     o.wgs_per_problem = int(wgs_per_problem)
     o.max_teams = int(max_teams)
     o.no_memo = (0 if speculate else 2) if memoize else 1
+    o.helpers = int(helpers)
     return o
 
 

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define FMPNP_ABI_VERSION 1
+#define FMPNP_ABI_VERSION 2
 
 /* robust losses, featurePnP/helpers/utils.py:15-78 */
 typedef enum {
@@ -78,6 +78,9 @@ typedef enum {
 #define FMPNP_STATUS_NAN 2               /* NaN step: model.py:411-413 (reference: NameError) */
 #define FMPNP_STATUS_NO_SUPPORT_TRIAL 4  /* no point inside at a trial pose: model.py:441-445 */
 #define FMPNP_STATUS_SYNC_TIMEOUT 8      /* internal: a cross-workgroup exchange timed out */
+#define FMPNP_STATUS_HELPER_WAIT 16      /* informational: a first-evaluation helper workgroup did not
+                                            publish in time and the main workgroup gathered that block
+                                            itself (results unaffected: same gather code) */
 
 /* argument errors (negative return codes) */
 #define FMPNP_EINVAL -1
@@ -100,8 +103,9 @@ typedef struct {
     int max_teams;          /* cap on concurrently resident problem teams; 0 = auto */
     int no_memo;            /* 1: re-gather every point's texel at every evaluation (the
                                reference's data movement); 0 (default): re-gather only points
-                               whose texel changed (with a -DFMPNP_SPEC=1 build, also gather the
-                               texels points are predicted to move to next beside the LM tail);
+                               whose texel changed and, where the planner enables it, also gather
+                               the texels points are predicted to move to next beside the LM tail
+                               (speculation: on by default; -DFMPNP_SPEC=0 compiles it out);
                                2: memoised without speculation -- all bit-identical results.
                                FMPNP_BILINEAR: 0/2 keep each point's cell memo (the six sums as
                                quadratics over its 2x2 cell, rebuilt when the cell changes; same
@@ -109,6 +113,11 @@ typedef struct {
     int layout;             /* fmpnp_layout of every problem's feat */
     int sobel_flags;        /* FMPNP_LAYOUT_F: bit 0 normalized (/8), bit 1 replicate padding
                                (the flags fmpnp_pack_features would have been given) */
+    int helpers;            /* first-evaluation helper workgroups per problem (small batches with
+                               idle CUs): 0 = the planner's choice, < 0 = none (e.g. when other
+                               kernels share the device and could keep helpers from being
+                               resident: the main workgroups would wait up to 0.2 s for them),
+                               > 0 = at most this many.  Results do not depend on it. */
 } fmpnp_options;
 
 typedef struct {
@@ -229,6 +238,45 @@ int fmpnp_debug_stamps(unsigned long long *device_buf);
 
 /* Last launch geometry of this thread (for benches / tests). */
 int fmpnp_last_launch(int *teams, int *wgs_per_problem, int *grid, int *lds_bytes);
+
+/* LM kernel builds (fmpnp_launch_info.build) */
+#define FMPNP_BUILD_WIDE 1        /* 256-thread workgroups, one wave per SIMD (bilinear cell memo) */
+#define FMPNP_BUILD_LATENCY 2     /* 512-thread workgroups, one per CU */
+#define FMPNP_BUILD_THROUGHPUT 4  /* 256-thread workgroups, two per CU (batches >= 2 per CU) */
+
+/* LM kernel variants (fmpnp_launch_info.variant): which code paths are compiled into the
+ * kernel that ran -- the loss / sampling / layout specialisation, the speculative next-texel
+ * gathers (_SPEC) and the first-evaluation helpers' hand-off (_H) */
+#define FMPNP_VAR_NEAREST 0        /* any loss, nearest sampling, packed f/gx/gy (and compute_cost) */
+#define FMPNP_VAR_GM 1             /* Geman-McClure forward, nearest, packed */
+#define FMPNP_VAR_BILINEAR 2       /* bilinear cell memo */
+#define FMPNP_VAR_F_NEAREST 3      /* FMPNP_LAYOUT_F, any loss */
+#define FMPNP_VAR_F_GM 4           /* FMPNP_LAYOUT_F, Geman-McClure */
+#define FMPNP_VAR_BIL_DIRECT 5     /* bilinear, every point sampled every evaluation */
+#define FMPNP_VAR_GM_SPEC 6
+#define FMPNP_VAR_NEAREST_SPEC 7
+#define FMPNP_VAR_GM_SPEC_H 8
+#define FMPNP_VAR_NEAREST_SPEC_H 9
+#define FMPNP_VAR_GM_H 10
+#define FMPNP_VAR_NEAREST_H 11
+
+typedef struct {
+    int teams, wgs_per_problem, grid, lds_bytes;
+    int build;              /* FMPNP_BUILD_* */
+    int variant;            /* FMPNP_VAR_* */
+    int team;               /* 1: wgs_per_problem > 1 (cross-workgroup exchange compiled in) */
+    int ratio;              /* 1: the ratio-test specialisation */
+    int dtype;              /* fmpnp_dtype of the texels */
+    int helpers;            /* first-evaluation helper workgroups per problem */
+    int speculate;          /* speculative next-texel gathers enabled */
+} fmpnp_launch_info;
+
+/* The LM launch plan for these problems and options, without launching anything (needs
+ * the current device: CU count and occupancy).  Returns 0 or the launch's error code. */
+int fmpnp_plan(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt, fmpnp_launch_info *out);
+
+/* Plan of the last LM launch of this thread. */
+int fmpnp_last_launch_info(fmpnp_launch_info *out);
 
 #ifdef __cplusplus
 }

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     L = _lib.load()
     missing = [f for f in declared_functions() if not hasattr(L, f)]
     assert not missing, missing
-    assert L.fmpnp_abi_version() == 1
+    assert L.fmpnp_abi_version() == _lib.ABI_VERSION == 2
     assert b"gfx950" in L.fmpnp_build_info()
 
 
@@ -43,7 +43,7 @@ def test_library_is_a_gfx950_code_object():
 
 
 STRUCTS = {"fmpnp_options": _lib.Options, "fmpnp_problem": _lib.Problem, "fmpnp_result": _lib.Result,
-           "fmpnp_trace_entry": _lib.TraceEntry}
+           "fmpnp_trace_entry": _lib.TraceEntry, "fmpnp_launch_info": _lib.LaunchInfo}
 
 
 @pytest.mark.parametrize("name", sorted(STRUCTS))

@@ -220,3 +220,102 @@ def test_first_evaluation_helpers_fp64_storage(monkeypatch):
     assert base["best_cost"] == res["best_cost"] and base["texel_gathers"] == res["texel_gathers"]
     np.testing.assert_array_equal(tb["cost"], tr["cost"])
     np.testing.assert_array_equal(tb["n_supported"], tr["n_supported"])
+
+
+# ---------------------------------------------------------------------------
+# The EXACT launches bench.py times, at the launch shapes it times them (configs[2]'s per-GPU
+# share of 128 queries; the fixed total of 1024 on one GPU takes the same two-workgroups-per-CU
+# build as B = 512): the plan of each launch is asserted (grid, build, variant, no helpers), and a
+# spread subset of >= 32 queries is compared with its own oracle run, trace included.
+# ---------------------------------------------------------------------------
+def _bench_batch(B):
+    """bench.py's setup: query q = synth.problem_inputs(seed=q), packed fp32 f/gx/gy."""
+    probs = []
+    for q in range(B):
+        inp = synth.problem_inputs(512, 256, 240, 320, seed=q, device=DEV)
+        probs.append(packed_problem(inp))
+        del inp
+    return probs
+
+
+def _oracle_subset(qs, ratio):
+    def one(q):
+        return oracle_run(host_copy(synth.problem_inputs(512, 256, 240, 320, seed=q, device=DEV)), ratio=ratio)
+    with ThreadPoolExecutor(8) as ex:
+        return list(ex.map(one, qs))
+
+
+@pytest.mark.parametrize("B,ratio,build,variant", [(128, None, "latency", "GM_SPEC"),
+                                                   (128, 0.8, "latency", "GM_SPEC"),
+                                                   (512, None, "throughput", "GM")])
+def test_bench_launch_against_oracle(B, ratio, build, variant):
+    """The headline launch (B = 128: lm_kernel<float, latency, !team, ratio, VAR_GM_SPEC>, grid 128,
+    no first-evaluation helpers), its ratio-test form (input_configs/full_robotcar_08.gin:40), and
+    the throughput build of B >= 512 (the fixed_total_1024 leg), each as bench.py launches it
+    (AsyncBatch), against the oracle (featurePnP/model.py:300-486, n_iters = 50 of model.gin:5)."""
+    probs = _bench_batch(B)
+    opts = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, ratio_threshold=ratio, dtype=_lib.F32)
+    ab = rf.AsyncBatch(probs, opts)
+    ab.launch()
+    res_async = ab.results()
+    info = _lib.last_launch()
+    assert (info["grid"], info["wgs_per_problem"], info["helpers"]) == (B, 1, 0), info
+    assert (info["build_name"], info["variant_name"], info["ratio"], info["dtype_name"]) == \
+        (build, variant, int(ratio is not None), "f32"), info
+    # the traced synchronous launch of the same batch: same plan, same poses bit for bit
+    res, trs = rf.refine(probs, opts, trace=True)
+    info2 = _lib.last_launch()
+    assert {k: info2[k] for k in ("grid", "build", "variant", "helpers", "team")} == \
+        {k: info[k] for k in ("grid", "build", "variant", "helpers", "team")}
+    for q in range(B):
+        assert np.array_equal(res[q]["R"], res_async[q]["R"]) and np.array_equal(res[q]["t"], res_async[q]["t"]), q
+        assert res[q]["n_evals"] == res_async[q]["n_evals"] and res[q]["status"] == res_async[q]["status"] == 0
+    del probs
+    qs = list(range(0, B, B // 32))  # 32 queries spread over the batch
+    for q, (ores, otr) in zip(qs, _oracle_subset(qs, ratio)):
+        check(res[q], trs[q], ores, otr, f"B={B} ratio={ratio} query {q}")
+
+
+def test_helpers_on_a_reused_workspace(monkeypatch):
+    """the first-evaluation helpers' records live in the launch workspace.  Batch A
+    then batch B (other maps, other points) on ONE reused workspace with helpers on must give B's
+    helpers-off results bit for bit -- no record of A can be taken for B's (launch-unique tags,
+    release/acquire hand-off, texel check)."""
+    mk = lambda seeds: [packed_problem(synth.problem_inputs(512, 256, 240, 320, seed=s, device=DEV, init="hard"))
+                        for s in seeds]
+    pa, pb = mk(range(60, 64)), mk(range(70, 74))
+    o = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32)
+    monkeypatch.setenv("FMPNP_HELPERS", "0")
+    base, tb = rf.refine(pb, o, trace=True)
+    monkeypatch.setenv("FMPNP_HELPERS", "1")
+    ab_a, ab_b = rf.AsyncBatch(pa, o), rf.AsyncBatch(pb, o)
+    ab_b.d_ws = ab_a.d_ws  # one workspace for both batches
+    ab_b.ws_bytes = ab_a.ws_bytes
+    for _ in range(3):
+        ab_a.launch()
+        ab_b.launch()
+        assert _lib.last_launch()["helpers"] > 0
+        got = ab_b.results()
+        for q in range(len(pb)):
+            assert np.array_equal(got[q]["R"], base[q]["R"]) and np.array_equal(got[q]["t"], base[q]["t"]), q
+            assert got[q]["best_cost"] == base[q]["best_cost"] and got[q]["n_evals"] == base[q]["n_evals"]
+            assert got[q]["texel_gathers"] == base[q]["texel_gathers"] and got[q]["status"] == 0
+
+
+def test_helpers_that_never_publish_change_nothing(monkeypatch):
+    """A helper that never publishes (FMPNP_DBG bit 3: the state a helper kept from being resident
+    leaves): every main workgroup waits its bounded 0.2 s per block, gathers the block itself and
+    reports FMPNP_STATUS_HELPER_WAIT; poses, costs and the schedule are bit-identical."""
+    prob = packed_problem(synth.problem_inputs(512, 256, 240, 320, seed=81, device=DEV, init="hard"))
+    o = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32)
+    monkeypatch.setenv("FMPNP_HELPERS", "0")
+    (base,), (tb,) = rf.refine([prob], o, trace=True)
+    monkeypatch.setenv("FMPNP_HELPERS", "1")
+    monkeypatch.setenv("FMPNP_DBG", "8")
+    (res,), (tr,) = rf.refine([prob], o, trace=True)
+    assert _lib.last_launch()["helpers"] > 0
+    assert res["status"] == _lib.STATUS_HELPER_WAIT and base["status"] == 0
+    assert np.array_equal(base["R"], res["R"]) and np.array_equal(base["t"], res["t"])
+    assert base["best_cost"] == res["best_cost"] and base["texel_gathers"] == res["texel_gathers"]
+    np.testing.assert_array_equal(tb["cost"], tr["cost"])
+    np.testing.assert_array_equal(tb["n_supported"], tr["n_supported"])

@@ -111,3 +111,44 @@ def test_two_rank_gloo_matches_single_process():
     assert len(res) == n
     for a, b in zip(res, single):
         assert a["R"] == b["R"] and a["t"] == b["t"] and a["best_cost"] == b["best_cost"]
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, env_extra, timeout=240):
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    return r.returncode, lines, r.stderr
+
+
+def test_bench_gpus_n_starts_n_ranks():
+    """`python bench.py --gpus 2` (the driver's form, no launcher) starts two rank processes
+    itself; each sees WORLD_SIZE 2 and takes its own block of queries (dry run: no GPU)."""
+    rc, lines, err = _bench(["--gpus", "2", "--batch", "3"], {"FMPNP_BENCH_DRYRUN": "1"})
+    assert rc == 0, err
+    assert sorted(d["rank"] for d in lines) == [0, 1]
+    assert all(d["world"] == 2 for d in lines)
+    by_rank = {d["rank"]: d["queries"] for d in lines}
+    assert by_rank[0] + by_rank[1] == list(range(6))
+
+
+def test_bench_strong_form_splits_the_total():
+    rc, lines, err = _bench(["--gpus", "2", "--global-batch", "5"], {"FMPNP_BENCH_DRYRUN": "1"})
+    assert rc == 0, err
+    by_rank = {d["rank"]: d["queries"] for d in lines}
+    assert by_rank[0] + by_rank[1] == list(range(5))
+
+
+def test_bench_refuses_a_rank_count_other_than_gpus():
+    """Under a launcher, --gpus must equal WORLD_SIZE: never report an n_gpus other than the
+    ranks that actually ran."""
+    rc, lines, err = _bench(["--gpus", "2"], {"WORLD_SIZE": "3", "RANK": "0", "FMPNP_BENCH_DRYRUN": "1"})
+    assert rc == 2 and not lines
+    assert "WORLD_SIZE" in err
