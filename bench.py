@@ -53,7 +53,7 @@ N_PTS, C, HF, WF, ITERS = 512, 256, 240, 320, 50
 HBM_PEAK = 8.0e12  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 B_ITER = N_PTS * (16 * C + 24)  # SURVEY.md §8d bytes per GN iteration per query (every point re-read)
 LEGS = ["single", "hard", "ratio", "no_spec", "no_memo", "bilinear", "layout_f", "pack", "pipeline", "fixed1024",
-        "cpu"]
+        "pyramid1664", "cpu"]
 
 
 def parse():
@@ -398,6 +398,8 @@ def run_legs(args, dev, probs, feats, inputs, opts, res_main, rf, _lib, synth):
         out.update(pack_legs(dev, _lib, synth))
     if "pipeline" in args.legs:
         out["end_to_end"] = pipeline_leg(dev, synth)
+    if "pyramid1664" in args.legs:
+        out["pyramid_robotcar_1664"] = pyramid_leg(dev, rf, synth, _lib, stream)
     if "fixed1024" in args.legs and B < 1024 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         out["fixed_total_1024"] = fixed_total_leg(args, dev, probs, feats, inputs, opts, rf, synth, stream)
     if "cpu" in args.legs and int(os.environ.get("WORLD_SIZE", "1")) == 1:
@@ -433,6 +435,44 @@ def fixed_total_leg(args, dev, probs, feats, inputs, opts, rf, synth, stream):
     del ps
     torch.cuda.empty_cache()
     return d
+
+
+def pyramid_leg(dev, rf, synth, _lib, stream, B=32):
+    """The reference's production refinement: RobotCar hypercolumns of C = 1664 channels
+    (network.gin:18) at 256x256 for a 1024x1024 image, 866 points per query (the largest
+    num_final_matches of results/results_s2dhm/robotcar/summary.csv), Geman-McClure, 50 iterations
+    per level over the channel pyramid of input_configs/default_robotcar.gin:75
+    [(640,1664), (128,640), (0,128)] (multilevel_optimization, model.py:178-213).  B queries per
+    launch, one launch per level, each level starting from the previous level's poses."""
+    levels = [(640, 1664), (128, 640), (0, 128)]
+    torch.cuda.synchronize()
+    feats, frefs, inps = [], [], []
+    for q in range(B):
+        inp = synth.problem_inputs(866, 1664, 256, 256, seed=20000 + q, device=dev, init="easy")
+        feats.append(rf.pack_features(inp.pop("fmap"), storage=torch.float32, device=dev))
+        frefs.append(inp.pop("fref"))
+        inps.append(inp)
+    R = [i["R0"] for i in inps]
+    t = [i["t0"] for i in inps]
+    opts = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32)
+    per_level, total = [], 0.0
+    for cb, ce in levels:
+        ps = [rf.make_problem(feats[q], frefs[q], inps[q]["pts3d"], inps[q]["K"], inps[q]["im_width"],
+                              inps[q]["im_height"], R[q], t[q], c_begin=cb, c_end=ce) for q in range(B)]
+        ms, res = time_launches(rf.AsyncBatch(ps, opts), 10, stream)
+        total += ms
+        per_level.append({"channels": [cb, ce], "ms_per_launch": round(ms, 4), "launch": _lib.last_launch(),
+                          "statuses": sorted({r["status"] for r in res}),
+                          "texel_gathers_per_point_eval": round(sum(r["texel_gathers"] for r in res) /
+                                                                max(1, 866 * sum(r["n_evals"] for r in res)), 4)})
+        R = [r["R"] for r in res]
+        t = [r["t"] for r in res]
+    del feats, frefs
+    torch.cuda.empty_cache()
+    return {"queries": B, "ms_per_batch": round(total, 4), "pose_refinements_per_s": round(B / (total / 1e3), 1),
+            "levels": per_level,
+            "workload": "C=1664 256x256 hypercolumns, 1024x1024 image, 866 points, GM, 50 iters per level, "
+                        "default_robotcar.gin:75 channel pyramid; sum of the three level launches"}
 
 
 def pack_legs(dev, _lib, synth):
