@@ -280,6 +280,36 @@ __host__ __device__ __forceinline__ void sincos_small(double x, double &s, doubl
     c = fma(z, pc, 1.0);
 }
 
+// The three even functions of a rotation angle theta that so3exp_map needs, as polynomials in
+// z = theta^2 (no square root, no division) for 0 <= z <= (pi/4)^2: cos theta, sin(theta)/theta and
+// (1 - cos theta)/theta^2 (Horner-form Taylor series, truncation below 1e-19 relative).  With
+// W = [w]x of the unnormalised axis-angle w (|w| = theta), W^2 = w w^T - theta^2 I, so
+// helpers/utils.py:209-221's I + sin(theta) [w/theta]x + (1 - cos theta) [w/theta]x^2 is
+// cos(theta) I + (sin(theta)/theta) W + ((1 - cos theta)/theta^2) w w^T.
+__host__ __device__ __forceinline__ void so3_coeffs_small(double z, double &c, double &a, double &b) {
+    double pc = kc(1.0 / 6402373705728000.0);       // 1/18!
+    pc = fma(pc, -z, kc(1.0 / 20922789888000.0));  // 1/16!
+    pc = fma(pc, -z, kc(1.0 / 87178291200.0));
+    pc = fma(pc, -z, kc(1.0 / 479001600.0));
+    pc = fma(pc, -z, kc(1.0 / 3628800.0));
+    pc = fma(pc, -z, kc(1.0 / 40320.0));
+    pc = fma(pc, -z, kc(1.0 / 720.0));
+    pc = fma(pc, -z, kc(1.0 / 24.0));
+    pc = fma(pc, -z, 0.5);                           // b = sum (-z)^k / (2k+2)!, k = 0..8
+    b = pc;
+    c = fma(pc, -z, 1.0);                            // cos = 1 - z b
+    double pa = kc(1.0 / 121645100408832000.0);     // 1/19!
+    pa = fma(pa, -z, kc(1.0 / 355687428096000.0));  // 1/17!
+    pa = fma(pa, -z, kc(1.0 / 1307674368000.0));
+    pa = fma(pa, -z, kc(1.0 / 6227020800.0));
+    pa = fma(pa, -z, kc(1.0 / 39916800.0));
+    pa = fma(pa, -z, kc(1.0 / 362880.0));
+    pa = fma(pa, -z, kc(1.0 / 5040.0));
+    pa = fma(pa, -z, kc(1.0 / 120.0));
+    pa = fma(pa, -z, kc(1.0 / 6.0));
+    a = fma(pa, -z, 1.0);                            // sin(theta)/theta
+}
+
 // The library sincos for the huge-angle branch below, out of line: its constant tables stay
 // inside the call and never occupy registers of the caller's hot loop.
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -49,6 +49,13 @@
 namespace fmpnp {
 
 constexpr bool kSpecBuild = FMPNP_SPEC != 0;
+// Debug instrumentation (fmpnp_debug_stamps: phase totals, per-evaluation stamps, the evaluation
+// timeline) is compiled in only with -DFMPNP_STAMPS=1 (a diagnostics build, tools/build_ab.sh):
+// its flags and pointers would otherwise hold scalar registers across the evaluation loop.
+#ifndef FMPNP_STAMPS
+#define FMPNP_STAMPS 0
+#endif
+constexpr bool kStamps = FMPNP_STAMPS != 0;
 
 // dynamic LDS of the LM kernel (the only kernel in this file that uses LDS)
 extern __shared__ __attribute__((aligned(16))) unsigned char lm_lds[];
@@ -84,7 +91,10 @@ struct Ctx {
 // -- each LDS read is a ~100-cycle round trip on the evaluation's critical path.
 struct PC {
     const void *feat, *fref;
-    double K[9];
+    // K: a pinhole matrix [[fx, 0, cx], [0, fy, cy], [0, 0, 1]] (kstd; the reference's intrinsics)
+    // keeps only its four parameters in scalar registers; any other K is read from the LDS Ctx
+    double fx, cx, fy, cy;
+    int kstd;
     int Hf, Wf, cs, cb, ce, ld, im_w, im_h, p0, M, c0, LC, G;
     UDiv dh, dw;
     int loss, no_memo, use_ratio, bilinear;
@@ -104,6 +114,11 @@ struct PC {
     double *part_g;       // this team's partial slots [2][nc_max][NV] (G > 1)
     int nc_max;
     bool stamps;          // debug phase stamps on
+    // debug timeline (FMPNP_DBG bit 4, evaluation FMPNP_DBG >> 8): absolute s_memtime of each
+    // wave at the tl_stamp sites of one evaluation of the team's first problem, [8][16] per WG
+    unsigned long long *tl;
+    int tl_eval, cur_eval;
+    int cur_ev;             // the evaluation being run (its pose is Ret[cur_ev & 1], its state sc[cur_ev & 1])
 };
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -127,15 +142,25 @@ __device__ __forceinline__ P *ufirst(P *p) {
     return (P *)(((uintptr_t)hi << 32) | lo);
 }
 
-struct LMState {
-    double tot[NV];         // reduced totals of the last evaluation (lane-written by wave 0)
-    double hc[NV];          // cached linearisation at (R, t): H upper triangle, then g
-    double R[9], t[3];      // current (last accepted) pose
-    double Re[9], te[3];    // pose evaluated next
-    double Rb[9], tb[3];    // best pose
-    double lambda, lr, prev, best, initial, rho_max;
+// The LM schedule's scalar state (model.py:281-283,347-359,469-486).  Two copies: evaluation k
+// reads sc[k & 1] and its tail writes sc[(k + 1) & 1], so the tail's waves (lm_tail_split) read
+// the state before the evaluation while one of them writes the next.
+struct LMScal {
+    double lambda, lr, prev, best, initial;
     int best_inl, n_evals, n_steps, n_accepted, status, done, has_best, ret_current;
+    int nan;                // a step came out NaN (model.py:411-413): written by the stepping wave only
+};
+constexpr int TAIL_ROLES = 3;  // tail waves of the split tail: accept stepper, reject stepper, bookkeeper
+struct LMState {
+    double tot[TAIL_ROLES][NV];  // each tail wave's combined totals of the evaluation (broadcast operands)
+    double hc[NV];          // cached linearisation at (R, t): H upper triangle, then g
+    double Rt[12];          // current (last accepted) pose [R | t]
+    double Ret[2][12];      // pose [R | t] evaluated by evaluation k: Ret[k & 1]
+    double Rbt[12];         // best pose
+    LMScal sc[2];
+    double rho_max;
     int abort_flag, sync_ok;
+    unsigned long long tlb[NT / 64][16];  // debug timeline (FMPNP_DBG bit 4), flushed at problem end
     double wg_max[NT / 64];
     unsigned long long bil_dirty[BIL_MAX_M / 64];  // bilinear memo: each block's points whose cell changed
     long long wg_gath[NT / 64];                     // per-wave texel gathers of the problem (G = 1)
@@ -152,8 +177,11 @@ __device__ __forceinline__ PC load_pc() {
     PC q;
     q.feat = ufirst(c.feat);
     q.fref = ufirst(c.fref);
-#pragma unroll
-    for (int k = 0; k < 9; ++k) q.K[k] = ufirst(c.K[k]);
+    q.fx = ufirst(c.K[0]);
+    q.cx = ufirst(c.K[2]);
+    q.fy = ufirst(c.K[4]);
+    q.cy = ufirst(c.K[5]);
+    q.kstd = ufirst((c.K[1] == 0.0 && c.K[3] == 0.0 && c.K[6] == 0.0 && c.K[7] == 0.0 && c.K[8] == 1.0) ? 1 : 0);
     q.Hf = ufirst(c.Hf); q.Wf = ufirst(c.Wf); q.cs = ufirst(c.cs); q.cb = ufirst(c.cb); q.ce = ufirst(c.ce);
     q.ld = ufirst(c.ld_ref); q.im_w = ufirst(c.im_w); q.im_h = ufirst(c.im_h); q.p0 = ufirst(c.p0);
     q.M = ufirst(c.M); q.c0 = ufirst(c.c0); q.LC = ufirst(c.LC); q.G = ufirst(c.G);
@@ -176,19 +204,50 @@ __device__ __forceinline__ PC load_pc() {
     q.sob_rep = ufirst((c.sobel_flags >> 1) & 1);
     q.part_g = ufirst(c.part_g);
     q.nc_max = ufirst(c.nc_max);
-    q.stamps = ufirst(c.stamps_on) != 0;
+    q.stamps = kStamps && ufirst(c.stamps_on) != 0;
+    q.tl = nullptr;
+    q.tl_eval = q.cur_eval = -1;
+    q.cur_ev = 0;
     return q;
 }
 // debug: add the cycles since the wave's previous stamp to its phase k (lane 0 of each
 // wave); phases 0..3 of the first evaluation go to slots 8..11
 __device__ __forceinline__ void dbg_stamp(bool on, int k) {
     LMState &st = *reinterpret_cast<LMState *>(lm_lds);
-    if (on && (threadIdx.x & 63) == 0) {
+    if (kStamps && on && (threadIdx.x & 63) == 0) {
         const int w = threadIdx.x >> 6;
         const unsigned long long now = __builtin_amdgcn_s_memtime();
-        st.stamp_ph[w][k < 4 && st.n_evals == 0 ? 8 + k : k] += now - st.stamp_t[w];
+        st.stamp_ph[w][k < 4 && st.sc[1].n_evals == 0 ? 8 + k : k] += now - st.stamp_t[w];
         st.stamp_t[w] = now;
     }
+}
+__device__ __forceinline__ void tl_stamp(const PC &q, int k) {
+    if (kStamps && q.tl && q.cur_eval == q.tl_eval && (threadIdx.x & 63) == 0)
+        reinterpret_cast<LMState *>(lm_lds)->tlb[threadIdx.x >> 6][k] = __builtin_amdgcn_s_memtime();
+}
+// project_px (fmpnp_device.h) for the problem's K.  With a pinhole K the products of its zero
+// entries are dropped: (fx P0 + 0 P1) + cx P2 equals fx P0 + cx P2 and (0 P0 + 0 P1) + 1 P2
+// equals P2 except in the sign of a zero or for a non-finite coordinate, and each of those makes
+// the quotient non-finite or rounds the pixel to -1 either way -- the point is unsupported in
+// both forms, so the support set and every pixel are the reference's.
+__device__ __forceinline__ bool project_pc(const PC &q, const double P[3], int &x, int &y, double &qx, double &qy) {
+    if (q.kstd) {
+#pragma clang fp contract(off)
+        const double u0 = q.fx * P[0] + q.cx * P[2];
+        const double u1 = q.fy * P[1] + q.cy * P[2];
+        qx = u0 / P[2];
+        qy = u1 / P[2];
+        const double px = rint(qx) - 1.0, py = rint(qy) - 1.0;
+        if (!(px >= 0.0 && px < (double)q.im_w && py >= 0.0 && py < (double)q.im_h)) return false;
+        x = (int)px;
+        y = (int)py;
+        return true;
+    }
+    const double *Kl = reinterpret_cast<const LMState *>(lm_lds)->c.K;  // broadcast reads (rare: non-pinhole K)
+    double K[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) K[k] = Kl[k];
+    return project_px(K, P, q.im_w, q.im_h, x, y, qx, qy);
 }
 __device__ __forceinline__ unsigned char *dyn() { return lm_lds + lds_fixed_bytes(); }
 // dynamic carve (mmax = max local points, a multiple of CH), structure of arrays with the
@@ -223,30 +282,49 @@ __device__ __forceinline__ double *lds_part(int mmax, bool spec) {
 __device__ __forceinline__ double *lds_memo(int mmax, int nc_max) { return lds_part(mmax, false) + (size_t)nc_max * NV; }
 
 // so3exp_map (helpers/utils.py:209-221) and the update R' = dR R, t' = dR t + dt
-// (model.py:416-426).
+// (model.py:416-426).  Steps up to 45 degrees (every LM step in practice) take the sqrt- and
+// division-free form dR = cos(theta) I + (sin(theta)/theta) W + ((1 - cos theta)/theta^2) w w^T
+// (so3_coeffs_small: three independent polynomials in z = |w|^2, a short dependency chain on the
+// LM tail); larger steps the reference's normalised form.
 __device__ __forceinline__ void pose_update(const double *R, const double *t, const double delta[6], double *Rn,
                                             double *tn) {
     const double w0 = delta[3], w1 = delta[4], w2 = delta[5];
-    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+    const double z = fma(w2, w2, fma(w1, w1, w0 * w0));
     double dR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-    if (isnan(theta)) {
+    if (isnan(z)) {
 #pragma unroll
         for (int i = 0; i < 9; ++i) dR[i] = NAN;
-    } else if (!(theta < 1e-12)) {
-        const double it = 1.0 / theta;  // w / theta within 1 ulp, one division instead of three
-        const double k0 = w0 * it, k1 = w1 * it, k2 = w2 * it;
-        const double W[9] = {0, -k2, k1, k2, 0, -k0, -k1, k0, 0};
-        double s, c;
-        if (theta <= 0.78539816339744828) sincos_small(theta, s, c);
-        else sincos_rr(theta, s, c);
-        const double c1 = 1.0 - c;
+    } else if (!(z < 1e-24)) {  // theta >= 1e-12 (below: the identity, as the reference)
+        if (z <= 0.61685027506808487) {  // (pi/4)^2
+            double cz, az, bz;
+            so3_coeffs_small(z, cz, az, bz);
+            const double bw0 = bz * w0, bw1 = bz * w1, bw2 = bz * w2;
+            const double aw0 = az * w0, aw1 = az * w1, aw2 = az * w2;
+            dR[0] = fma(bw0, w0, cz);
+            dR[1] = fma(bw0, w1, -aw2);
+            dR[2] = fma(bw0, w2, aw1);
+            dR[3] = fma(bw1, w0, aw2);
+            dR[4] = fma(bw1, w1, cz);
+            dR[5] = fma(bw1, w2, -aw0);
+            dR[6] = fma(bw2, w0, -aw1);
+            dR[7] = fma(bw2, w1, aw0);
+            dR[8] = fma(bw2, w2, cz);
+        } else {
+            const double theta = sqrt(z);
+            const double it = 1.0 / theta;
+            const double k0 = w0 * it, k1 = w1 * it, k2 = w2 * it;
+            const double W[9] = {0, -k2, k1, k2, 0, -k0, -k1, k0, 0};
+            double sn, cs;
+            sincos_rr(theta, sn, cs);
+            const double c1 = 1.0 - cs;
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
+            for (int i = 0; i < 3; ++i)
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                double ww = W[3 * i + 0] * W[0 + j] + W[3 * i + 1] * W[3 + j] + W[3 * i + 2] * W[6 + j];
-                dR[3 * i + j] += W[3 * i + j] * s + ww * c1;
-            }
+                for (int j = 0; j < 3; ++j) {
+                    double ww = W[3 * i + 0] * W[0 + j] + W[3 * i + 1] * W[3 + j] + W[3 * i + 2] * W[6 + j];
+                    dR[3 * i + j] += W[3 * i + j] * sn + ww * c1;
+                }
+        }
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -345,17 +423,20 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
         c.p0 = c.c0 * CH;
         c.M = max(min(c1 * CH, c.N) - c.p0, 0);
         c.vec = 0;
-        for (int k = 0; k < 9; ++k) { st.R[k] = st.Re[k] = st.Rb[k] = pb->R0[k]; }
-        for (int k = 0; k < 3; ++k) { st.t[k] = st.te[k] = st.tb[k] = pb->t0[k]; }
-        st.lambda = c.lambda0;
-        st.lr = 1.0;
-        st.prev = st.best = st.initial = NAN;
-        st.best_inl = -1;
-        st.n_evals = st.n_steps = st.n_accepted = 0;
-        st.status = c.dead ? FMPNP_STATUS_SYNC_TIMEOUT : 0;
-        st.has_best = 0;
-        st.ret_current = 0;
-        st.done = c.dead || (c.mode != FMPNP_MODE_COMPUTE_COST && c.n_iters <= 0);
+        for (int k = 0; k < 12; ++k) st.Rt[k] = st.Ret[0][k] = st.Rbt[k] = k < 9 ? pb->R0[k] : pb->t0[k - 9];
+        for (int par = 0; par < 2; ++par) {
+            LMScal &sc = st.sc[par];
+            sc.lambda = c.lambda0;
+            sc.lr = 1.0;
+            sc.prev = sc.best = sc.initial = NAN;
+            sc.best_inl = -1;
+            sc.n_evals = sc.n_steps = sc.n_accepted = 0;
+            sc.status = c.dead ? FMPNP_STATUS_SYNC_TIMEOUT : 0;
+            sc.has_best = 0;
+            sc.ret_current = 0;
+            sc.done = c.dead || (c.mode != FMPNP_MODE_COMPUTE_COST && c.n_iters <= 0);
+            sc.nan = 0;
+        }
         st.abort_flag = 0;
     }
     __syncthreads();
@@ -368,6 +449,7 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
     for (int e = tid; e < 3 * c.M; e += nt) X[(e % 3) * rs + e / 3] = src[e];
     int *tex = lds_tex(mmax, c.spec);
     for (int i = tid; i < mmax; i += nt) tex[i] = -2;  // no texel cached yet
+    for (int i = tid; i < (NT / 64) * 16; i += nt) st.tlb[i >> 4][i & 15] = 0;  // debug timeline
     if (c.spec) {
         int *tex2 = lds_tex2(mmax, true), *slot = lds_slot(mmax, true), *spec = lds_spec(mmax, true);
         float *qp = lds_qp(mmax, true);
@@ -381,28 +463,33 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
     __syncthreads();
 }
 
-__device__ __forceinline__ void problem_end(bool own_gathers) {
+// k: the evaluations completed (the state is sc[k & 1])
+__device__ __forceinline__ void problem_end(bool own_gathers, int k, unsigned long long *tl) {
     LMState &st = S();
+    if (tl && (threadIdx.x & 63) == 0)  // debug timeline: this wave's stamps
+        for (int j = 0; j < 16; ++j) tl[(threadIdx.x >> 6) * 16 + j] = st.tlb[threadIdx.x >> 6][j];
     if (threadIdx.x == 0) {
+        LMScal &sc = st.sc[k & 1];
         if (st.abort_flag) {
             st.c.dead = 1;
-            st.status |= FMPNP_STATUS_SYNC_TIMEOUT;
+            sc.status |= FMPNP_STATUS_SYNC_TIMEOUT;
         }
+        if (sc.nan) sc.status |= FMPNP_STATUS_NAN;
         if (st.c.s == 0) {
             fmpnp_result &r = st.c.results[st.c.p];
-            const bool cur = st.ret_current || st.c.mode == FMPNP_MODE_COMPUTE_COST;
-            for (int k = 0; k < 9; ++k) r.R[k] = cur ? st.R[k] : st.Rb[k];
-            for (int k = 0; k < 3; ++k) r.t[k] = cur ? st.t[k] : st.tb[k];
-            r.initial_cost = st.initial;
-            r.best_cost = st.has_best ? st.best : NAN;
-            r.final_lambda = st.lambda;
-            r.final_lr = st.lr;
-            r.best_num_inliers = st.has_best ? st.best_inl : -1;
-            r.n_evals = st.n_evals;
-            r.n_steps = st.n_steps;
-            r.n_accepted = st.n_accepted;
-            r.status = st.status;
-            r.has_best = st.has_best;
+            const bool cur = sc.ret_current || st.c.mode == FMPNP_MODE_COMPUTE_COST;
+            for (int j = 0; j < 9; ++j) r.R[j] = cur ? st.Rt[j] : st.Rbt[j];
+            for (int j = 0; j < 3; ++j) r.t[j] = cur ? st.Rt[9 + j] : st.Rbt[9 + j];
+            r.initial_cost = sc.initial;
+            r.best_cost = sc.has_best ? sc.best : NAN;
+            r.final_lambda = sc.lambda;
+            r.final_lr = sc.lr;
+            r.best_num_inliers = sc.has_best ? sc.best_inl : -1;
+            r.n_evals = sc.n_evals;
+            r.n_steps = sc.n_steps;
+            r.n_accepted = sc.n_accepted;
+            r.status = sc.status;
+            r.has_best = sc.has_best;
             if (own_gathers) {
                 long long g = 0;
                 for (int w = 0; w < nwaves(); ++w) g += st.wg_gath[w];
@@ -613,7 +700,7 @@ __device__ __forceinline__ void contrib_block(const PC &q, int mmax, int blk, bo
                                               double d1, const double *r, int rs, const double Pc[3],
                                               double *dst_g) {
     const int lane = threadIdx.x & 63;
-    const double fx = q.K[0], fy = q.K[4];
+    const double fx = q.fx, fy = q.fy;
     const int lc = blk;  // one chunk per 64-point block
     const double w = kept ? d1 : 0.0, rh = kept ? rho : 0.0;
     const double P0 = kept ? Pc[0] : 0.0, P1 = kept ? Pc[1] : 0.0, z = kept ? Pc[2] : 1.0;
@@ -1538,10 +1625,11 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
     // the pose evaluated: one LDS broadcast read per evaluation, kept in VGPRs (moving it to
     // SGPRs costs 24 v_readfirstlane and SGPR spills)
     double Re[9], te[3];
+    const double *pev = st.Ret[q.cur_ev & 1];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Re[k] = st.Re[k];
+    for (int k = 0; k < 9; ++k) Re[k] = pev[k];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) te[k] = st.te[k];
+    for (int k = 0; k < 3; ++k) te[k] = pev[9 + k];
     double lmax = -1.0;  // -1: nothing supported seen yet
     for (int blk = wave; blk * 64 < M; blk += nwaves()) {
         const int i = blk * 64 + lane;
@@ -1572,7 +1660,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
             transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
             int x, y;
             double qx, qy;
-            if (project_px(q.K, Pc, q.im_w, q.im_h, x, y, qx, qy)) {
+            if (project_pc(q, Pc, x, y, qx, qy)) {
                 const int row = (int)udiv((unsigned)y * (unsigned)q.Hf, q.dh);
                 const int col = (int)udiv((unsigned)x * (unsigned)q.Wf, q.dw);
                 off = row * q.Wf + col;
@@ -1628,7 +1716,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
                 }
                 // a helper that never published (kept from being resident by other kernels): the
                 // block is gathered here as usual; reported, results unaffected
-                if (!ok) atomicOr(&st.status, FMPNP_STATUS_HELPER_WAIT);
+                if (!ok) atomicOr(&st.sc[0].status, FMPNP_STATUS_HELPER_WAIT);  // (the first evaluation's state)
             }
             if (__builtin_amdgcn_readfirstlane(ok)) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every lane: no record read above the poll
@@ -1646,6 +1734,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
             }
         }
         dbg_stamp(q.stamps, 0);
+        tl_stamp(q, 1);
         const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
         const bool wlane = (lane & 3) == 0 && e6 < 6;
         const size_t fo = (size_t)(wlane ? e6 : 0) * rs + blk * 64;  // this lane's field column
@@ -1660,6 +1749,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         // a wave complete in order; the clobber keeps the compiler from reordering them
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         dbg_stamp(q.stamps, 1);
+        tl_stamp(q, 2);
         const bool sup = off >= 0;
         const double *r = (sl ? rec2 : rec) + ii;  // the record slot in use
         double rho = 0.0, d1 = 0.0;
@@ -1674,6 +1764,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
             contrib_block(q, mmax, blk, sup, sup, rho, d1, r, rs, Pc, dst_g);
         }
         dbg_stamp(q.stamps, 2);
+        tl_stamp(q, 3);
     }
     return lmax;
 }
@@ -1713,16 +1804,17 @@ __device__ __forceinline__ double eval_pass_bil(const PC &q, int mmax, long long
     int key = -1;
     if (own) {
         double Re[9], te[3];
+        const double *pev = st.Ret[q.cur_ev & 1];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) Re[k] = st.Re[k];
+        for (int k = 0; k < 9; ++k) Re[k] = pev[k];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) te[k] = st.te[k];
+        for (int k = 0; k < 3; ++k) te[k] = pev[9 + k];
         const int old = valid ? tex[i] : -1;
         if (valid) {
             transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
             int x, y;
             double qx, qy;
-            if (project_px(q.K, Pc, q.im_w, q.im_h, x, y, qx, qy)) {
+            if (project_pc(q, Pc, x, y, qx, qy)) {
                 Taps tp;
                 bilinear_taps(qx, qy, q.Hf, q.Wf, q.im_w, q.im_h, tp);
                 key = tp.key;
@@ -1787,10 +1879,11 @@ __device__ __forceinline__ void contrib_pass(const PC &q, int mmax) {
     double *dst_g = q.part_g;
     if (q.G > 1) dst_g += (size_t)((ufirst((int)st.c.epoch) + 1) & 1) * q.nc_max * NV;
     double Re[9], te[3];
+    const double *pev = st.Ret[q.cur_ev & 1];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Re[k] = ufirst(st.Re[k]);
+    for (int k = 0; k < 9; ++k) Re[k] = ufirst(pev[k]);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) te[k] = ufirst(st.te[k]);
+    for (int k = 0; k < 3; ++k) te[k] = ufirst(pev[9 + k]);
     for (int blk = wave; blk * 64 < q.M; blk += nwaves()) {
         const int i = blk * 64 + lane;
         const bool valid = i < q.M;
@@ -1841,7 +1934,7 @@ __device__ __forceinline__ double combine_final_wave(int mmax, bool team) {
     double a = t, b = t;
     swap32(a, b);  // low half: (own, partner); high half: (partner, own)
     const double tot = a + b;  // even chunks + odd chunks, in both halves
-    if (lane < NV) st.tot[lane] = tot;  // for the solve's broadcast reads
+    if (lane < NV) st.tot[threadIdx.x >> 6][lane] = tot;  // this tail wave's copy, for its solve's broadcast reads
     return tot;
 }
 
@@ -1969,7 +2062,7 @@ __device__ __forceinline__ bool ldlt_step(const double *Hu, const double *g, dou
     for (int j = 5; j >= 0; --j) {
         double v = b[j] * inv[j];
 #pragma unroll
-        for (int i = j + 1; i < 6; ++i) v = fma(-a[i][j], x[i], v);
+        for (int i = 5; i > j; --i) v = fma(-a[i][j], x[i], v);  // x[j + 1], the newest, last: one fma per step
         x[j] = v;
     }
 #pragma unroll
@@ -1978,139 +2071,238 @@ __device__ __forceinline__ bool ldlt_step(const double *Hu, const double *g, dou
 }
 
 // ---------------------------------------------------------------------------
-// LM state machine (model.py:300-486) on wave 0.  The evaluation's totals arrive
-// lane-distributed (lane j holds value j, from the combine, which also stored them to
-// st.tot); the three the schedule needs are taken by v_readlane.  The scalar state and
-// this lane's pose elements (lane k < 12: R[k] for k < 9, t[k - 9]) are read in one LDS
-// burst; the pose and linearisation copies are lane-wise stores nothing waits on; the
-// solve and the pose update read their uniform operands by LDS broadcast.  Every team
-// member computes the same from identical totals.
+// LM state machine (model.py:300-486): the tail of evaluation k.  The evaluation's totals arrive
+// lane-distributed (lane j holds value j, from the combine, which also stored them to the wave's
+// st.tot row); the three the schedule needs are taken by v_readlane.
+//
+// The tail is the serial part of every evaluation (combine -> damped 6x6 solve -> pose update
+// -> next evaluation), and one wave issues it alone on its SIMD.  With one workgroup per problem
+// it is therefore split over three waves on three SIMDs, each of which combines the partials
+// itself (same fixed order: identical totals) and takes the accept / reject decision itself:
+//   role ACC   (wave 0) solves the evaluation's own normal equations with the accept branch's
+//              damping (model.py:469-478: lambda / 10 clipped, lr = 1; the first evaluation
+//              keeps lambda0) before the decision is known, and if the evaluation is accepted
+//              (or is the first) steps from the evaluated pose and stores the next pose;
+//   role REJ   (wave 1) solves the cached linearisation with the reject branch's damping
+//              (lambda * 10, lr / 10, clipped) and steps from the current pose if it is rejected;
+//   role BOOK  (wave 2) keeps the books: the schedule's scalars, best pose, the linearisation
+//              cache, the current pose, the trace.
+// The state before the evaluation is sc[k & 1] / Ret[k & 1] and the tail writes sc[(k+1) & 1] /
+// Ret[(k+1) & 1], so no tail wave reads what another one writes.  Same operands and code as a
+// decide-first tail: bit-identical steps.  Teams (G > 1, one polling wave) run every role on
+// wave 0 (ROLE_ALL) with the decision first.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void lm_update_wave(double tot, bool stamps) {
-    LMState &st = S();
-    const Ctx &c = st.c;
-    const int lane = threadIdx.x & 63;
-    const bool w0 = lane == 0;
-    const int kk = lane < 12 ? lane : 0;
-    static_assert(offsetof(LMState, Re) == offsetof(LMState, R) + 12 * sizeof(double), "R/t/Re/te layout");
-    static_assert(offsetof(LMState, hc) == offsetof(LMState, tot) + NV * sizeof(double), "tot/hc layout");
-    // LDS burst: scalar state and this lane's evaluated pose element
-    const double lam_s = st.lambda, lr_s = st.lr, prev = st.prev, best_s = st.best;
-    const int n_evals = st.n_evals, n_steps = st.n_steps;
-    const double pe = st.R[12 + kk];  // [Re | te][k]
-    const int mode = c.mode, n_iters = c.n_iters;
+constexpr int ROLE_ACC = 1, ROLE_REJ = 2, ROLE_BOOK = 4, ROLE_ALL = 7;
+
+struct Decision {
+    double cost, lambda, lr;
+    int kept, nsup;
+    bool first, accepted, take, new_best, stop;  // stop: no step follows (cost mode, no support, last)
+};
+
+__device__ __forceinline__ Decision lm_decide(double tot, const LMScal &s, int mode, int n_iters) {
+    Decision d;
     const double kept_d = rlane(tot, 28);
-    const int nsup = (int)rlane(tot, 29);
-    const int kept = (int)kept_d;
-    const double cost = rlane(tot, 27) / kept_d;  // torch mean of an empty tensor = NaN
-    if (mode == FMPNP_MODE_COMPUTE_COST) {
-        if (w0) {
-            st.initial = nsup == 0 ? NAN : cost;
-            if (nsup == 0) st.status |= FMPNP_STATUS_NO_SUPPORT;
-            st.n_evals = 1;
-            st.done = 1;
-        }
-        return;
-    }
-    const bool first = n_evals == 0;
-    if (nsup == 0) {  // model.py:316-320 / :441-445: return the current pose
-        if (w0) {
-            st.status |= first ? FMPNP_STATUS_NO_SUPPORT : FMPNP_STATUS_NO_SUPPORT_TRIAL;
-            st.ret_current = 1;
-            st.done = 1;
-        }
-        return;
-    }
-    double lambda = lam_s, lr = lr_s;
-    bool accepted = true;
-    if (!first) {  // model.py:469-478
-        accepted = !(cost > prev);
-        const double lam = lambda * (cost > prev ? 10.0 : 0.1);
-        lambda = lam < 1e-6 ? 1e-6 : (lam > 1e4 ? 1e4 : lam);
-        if (!accepted) {
-            const double l2 = 0.1 * lr;
-            lr = l2 < 1e-3 ? 1e-3 : (l2 > 1.0 ? 1.0 : l2);
+    d.nsup = (int)rlane(tot, 29);
+    d.kept = (int)kept_d;
+    d.cost = rlane(tot, 27) / kept_d;  // torch mean of an empty tensor = NaN
+    d.first = s.n_evals == 0;
+    d.lambda = s.lambda;
+    d.lr = s.lr;
+    d.accepted = true;
+    if (!d.first) {  // model.py:469-478
+        d.accepted = !(d.cost > s.prev);
+        const double lam = d.lambda * (d.cost > s.prev ? 10.0 : 0.1);
+        d.lambda = lam < 1e-6 ? 1e-6 : (lam > 1e4 ? 1e4 : lam);
+        if (!d.accepted) {
+            const double l2 = 0.1 * d.lr;
+            d.lr = l2 < 1e-3 ? 1e-3 : (l2 > 1.0 ? 1.0 : l2);
         } else {
-            lr = 1.0;
+            d.lr = 1.0;
         }
     }
     // the evaluated pose becomes current and its normal equations the linearisation
-    const bool take = first || accepted;
-    const bool new_best = !first && accepted && cost < best_s;
-    if (lane < 12) {
-        if (new_best) st.Rb[lane] = pe;  // [Rb | tb] contiguous
-        if (take) st.R[lane] = pe;       // [R | t]
-    }
-    if (take && lane < NV) st.hc[lane] = tot;
-    if (w0) {
-        if (first) {  // model.py:347-359
-            st.prev = st.best = st.initial = cost;
-            st.best_inl = kept;
-            st.has_best = 1;
-        } else if (accepted) {  // model.py:477-486
-            st.n_accepted++;
-            if (new_best) {
-                st.best_inl = kept;
-                st.best = cost;
-            }
-            st.prev = cost;
+    d.take = d.first || d.accepted;
+    d.new_best = !d.first && d.accepted && d.cost < s.best;
+    d.stop = mode == FMPNP_MODE_COMPUTE_COST || d.nsup == 0 || s.n_steps >= n_iters;
+    return d;
+}
+
+// The books of evaluation k: sc[nxt] from sc[cur] and the decision, the best / current pose, the
+// linearisation cache, the trace.  pe: this lane's element of the evaluated pose (lane < 12).
+__device__ __forceinline__ void lm_book(const Decision &d, double tot, double pe, int cur, int mode) {
+    LMState &st = S();
+    const Ctx &c = st.c;
+    const int lane = threadIdx.x & 63;
+    const LMScal &s = st.sc[cur];
+    LMScal &o = st.sc[cur ^ 1];
+    if (mode == FMPNP_MODE_COMPUTE_COST) {
+        if (lane == 0) {
+            o = s;
+            o.nan = 0;
+            o.initial = d.nsup == 0 ? NAN : d.cost;
+            if (d.nsup == 0) o.status |= FMPNP_STATUS_NO_SUPPORT;
+            o.n_evals = 1;
+            o.done = 1;
         }
-        st.lambda = lambda;
-        st.lr = lr;
-        st.n_evals = n_evals + 1;
-    }
-    if (c.trace && c.s == 0 && n_evals < c.trace_stride) {
-        fmpnp_trace_entry &e = c.trace[(size_t)c.p * c.trace_stride + n_evals];
-        if (lane < 9) e.R[lane] = pe;
-        else if (lane < 12) e.t[lane - 9] = pe;
-        if (w0) {
-            e.cost = cost;
-            e.lambda_after = lambda;
-            e.lr_after = lr;
-            e.n_supported = nsup;
-            e.n_kept = kept;
-            e.accepted = accepted ? 1 : 0;
-        }
-    }
-    if (n_steps >= n_iters) {
-        if (w0) st.done = 1;
         return;
     }
-    // next step from the linearisation at the current pose (model.py:408-426); uniform
-    // operands by LDS broadcast (this wave's own stores above: LDS is in order per wave)
-    const double *hs = st.tot + (take ? 0 : NV);
-    double Hu[21], gv[6], delta[6];
-#pragma unroll
-    for (int k = 0; k < 21; ++k) Hu[k] = hs[k];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) gv[k] = hs[21 + k];
-    dbg_stamp(stamps, 5);  // LM bookkeeping
+    if (d.nsup == 0) {  // model.py:316-320 / :441-445: return the current pose
+        if (lane == 0) {
+            o = s;
+            o.nan = 0;
+            o.status |= d.first ? FMPNP_STATUS_NO_SUPPORT : FMPNP_STATUS_NO_SUPPORT_TRIAL;
+            o.ret_current = 1;
+            o.done = 1;
+        }
+        return;
+    }
+    if (lane < 12) {
+        if (d.new_best) st.Rbt[lane] = pe;
+        if (d.take) st.Rt[lane] = pe;
+    }
+    if (d.take && lane < NV) st.hc[lane] = tot;
+    if (lane == 0) {
+        LMScal n = s;
+        if (d.first) {  // model.py:347-359
+            n.prev = n.best = n.initial = d.cost;
+            n.best_inl = d.kept;
+            n.has_best = 1;
+        } else if (d.accepted) {  // model.py:477-486
+            n.n_accepted++;
+            if (d.new_best) {
+                n.best_inl = d.kept;
+                n.best = d.cost;
+            }
+            n.prev = d.cost;
+        }
+        n.lambda = d.lambda;
+        n.lr = d.lr;
+        n.n_evals = s.n_evals + 1;
+        if (d.stop) n.done = 1;
+        else n.n_steps = s.n_steps + 1;  // the step is taken (a NaN step counts, model.py:411-413)
+        // (nan is the stepping wave's: never written here)
+        o.lambda = n.lambda;
+        o.lr = n.lr;
+        o.prev = n.prev;
+        o.best = n.best;
+        o.initial = n.initial;
+        o.best_inl = n.best_inl;
+        o.n_evals = n.n_evals;
+        o.n_steps = n.n_steps;
+        o.n_accepted = n.n_accepted;
+        o.status = n.status;
+        o.done = n.done;
+        o.has_best = n.has_best;
+        o.ret_current = n.ret_current;
+    }
+    if (c.trace && c.s == 0 && s.n_evals < c.trace_stride) {
+        fmpnp_trace_entry &e = c.trace[(size_t)c.p * c.trace_stride + s.n_evals];
+        if (lane < 9) e.R[lane] = pe;
+        else if (lane < 12) e.t[lane - 9] = pe;
+        if (lane == 0) {
+            e.cost = d.cost;
+            e.lambda_after = d.lambda;
+            e.lr_after = d.lr;
+            e.n_supported = d.nsup;
+            e.n_kept = d.kept;
+            e.accepted = d.accepted ? 1 : 0;
+        }
+    }
+}
+
+// One step: delta from the damped system hs (21 + 6 doubles in LDS, already in Hu / gv when
+// `solved` tells whether the LDL^T fast path succeeded), pose update from base, next pose stored.
+__device__ __forceinline__ void lm_step_store(const double *hs, double delta[6], bool solved, double lambda,
+                                              double lr, const double *base, int nxt) {
+    LMState &st = S();
+    const int lane = threadIdx.x & 63;
     // (the pivoted-LU fallback indexes H by lane: it reads the LDS copy, not a private array)
-    if (!ldlt_step(Hu, gv, lambda, lr, delta)) lm_step_rows(hs, hs + 21, lambda, lr, delta);
-    dbg_stamp(stamps, 6);  // 6x6 solve
+    if (!solved) lm_step_rows(hs, hs + 21, lambda, lr, delta);
     bool bad = false;
 #pragma unroll
     for (int k = 0; k < 6; ++k) bad |= isnan(delta[k]);
     if (bad) {  // model.py:411-413
-        if (w0) {
-            st.n_steps = n_steps + 1;
-            st.status |= FMPNP_STATUS_NAN;
-            st.done = 1;
-        }
+        if (lane == 0) st.sc[nxt].nan = 1;
         return;
     }
-    const double *pp = st.R + (take ? 12 : 0);  // [R | t] or [Re | te]
     double Rc[9], tc[3], Rn[9], tn[3];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Rc[k] = pp[k];
+    for (int k = 0; k < 9; ++k) Rc[k] = base[k];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) tc[k] = pp[9 + k];
+    for (int k = 0; k < 3; ++k) tc[k] = base[9 + k];
     pose_update(Rc, tc, delta, Rn, tn);
-    if (w0) {
-        st.n_steps = n_steps + 1;
-        for (int k = 0; k < 9; ++k) st.Re[k] = Rn[k];
-        for (int k = 0; k < 3; ++k) st.te[k] = tn[k];
+    double *o = st.Ret[nxt];
+    if (lane == 0) {
+        for (int k = 0; k < 9; ++k) o[k] = Rn[k];
+        for (int k = 0; k < 3; ++k) o[9 + k] = tn[k];
     }
+}
+
+__device__ __forceinline__ double clip_lam(double l) { return l < 1e-6 ? 1e-6 : (l > 1e4 ? 1e4 : l); }
+__device__ __forceinline__ double clip_lr(double l) { return l < 1e-3 ? 1e-3 : (l > 1.0 ? 1.0 : l); }
+
+// One role (or all, ROLE_ALL) of the tail of evaluation k.  tot: this wave's combined totals.
+__device__ __forceinline__ void lm_tail(int role, double tot, const PC &q, int k) {
+    LMState &st = S();
+    const Ctx &c = st.c;
+    const int lane = threadIdx.x & 63;
+    const int cur = k & 1, nxt = cur ^ 1;
+    const int kk = lane < 12 ? lane : 0;
+    const LMScal &s = st.sc[cur];
+    const int mode = c.mode, n_iters = c.n_iters;
+    const double *row = st.tot[threadIdx.x >> 6];  // this wave's totals, as stored by its combine
+    if (role == ROLE_ALL) {
+        const Decision d = lm_decide(tot, s, mode, n_iters);
+        const double pe = st.Ret[cur][kk];
+        lm_book(d, tot, pe, cur, mode);
+        dbg_stamp(q.stamps, 5);  // LM bookkeeping
+        tl_stamp(q, 7);
+        if (d.stop) return;
+        const double *hs = d.take ? row : st.hc;
+        double Hu[21], gv[6], delta[6];
+#pragma unroll
+        for (int j = 0; j < 21; ++j) Hu[j] = hs[j];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) gv[j] = hs[21 + j];
+        const bool solved = ldlt_step(Hu, gv, d.lambda, d.lr, delta);
+        dbg_stamp(q.stamps, 6);  // 6x6 solve
+        tl_stamp(q, 8);
+        lm_step_store(hs, delta, solved, d.lambda, d.lr, d.take ? st.Ret[cur] : st.Rt, nxt);
+        return;
+    }
+    if (role == ROLE_BOOK) {
+        const Decision d = lm_decide(tot, s, mode, n_iters);
+        lm_book(d, tot, st.Ret[cur][kk], cur, mode);
+        return;
+    }
+    // a stepper: its branch's operands and damping are known before the decision.  Everything it
+    // reads from LDS -- the state, the step's base pose, the operands -- is read up front, so the
+    // chain after the combine is the solve and the pose update with no LDS round trip between.
+    const bool acc = role == ROLE_ACC;
+    const LMScal sv = s;
+    const bool first = sv.n_evals == 0;
+    if (!acc && first) return;  // the first evaluation is always taken
+    const double *basep = acc ? st.Ret[cur] : st.Rt;
+    double base[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) base[j] = basep[j];
+    const double *hs = acc ? row : st.hc;
+    const double lam = acc ? (first ? sv.lambda : clip_lam(sv.lambda * 0.1)) : clip_lam(sv.lambda * 10.0);
+    const double lr = acc ? (first ? sv.lr : 1.0) : clip_lr(0.1 * sv.lr);
+    double Hu[21], gv[6], delta[6];
+#pragma unroll
+    for (int j = 0; j < 21; ++j) Hu[j] = hs[j];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) gv[j] = hs[21 + j];
+    const bool solved = ldlt_step(Hu, gv, lam, lr, delta);
+    // (the step is formed here, not sunk past the decision's branch: the decision's instructions
+    // then fill the solve's dependency stalls instead of adding to them)
+    asm volatile("" ::"v"(delta[0]), "v"(delta[1]), "v"(delta[2]), "v"(delta[3]), "v"(delta[4]), "v"(delta[5]));
+    const Decision d = lm_decide(tot, sv, mode, n_iters);
+    if (d.stop || d.take != acc) return;
+    tl_stamp(q, 8);
+    lm_step_store(hs, delta, solved, lam, lr, base, nxt);
 }
 
 // ---------------------------------------------------------------------------
@@ -2136,9 +2328,9 @@ __device__ __forceinline__ void helper_run(const LaunchArgs &a, int mmax) {
     const int rs = lds_rs(mmax);
     double Re[9], te[3];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Re[k] = st.Re[k];
+    for (int k = 0; k < 9; ++k) Re[k] = st.Ret[0][k];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) te[k] = st.te[k];
+    for (int k = 0; k < 3; ++k) te[k] = st.Ret[0][9 + k];
     double *out = a.hrec + (size_t)p * a.nc_max * CH * HREC;
     const int nw = nwaves(), per = 64 / nw;
     for (int blk = hb; blk * 64 < q.M; blk += a.helpers) {
@@ -2150,7 +2342,7 @@ __device__ __forceinline__ void helper_run(const LaunchArgs &a, int mmax) {
             transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
             int x, y;
             double qx, qy;
-            if (project_px(q.K, Pc, q.im_w, q.im_h, x, y, qx, qy)) {
+            if (project_pc(q, Pc, x, y, qx, qy)) {
                 const int row = (int)udiv((unsigned)y * (unsigned)q.Hf, q.dh);
                 const int col = (int)udiv((unsigned)x * (unsigned)q.Wf, q.dw);
                 off = row * q.Wf + col;
@@ -2228,7 +2420,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
         c.dbg = a.dbg;
         c.sampling = a.opt.sampling;
         c.sobel_flags = a.opt.sobel_flags;
-        c.stamps_on = a.stamps != nullptr && !(a.dbg & 4);  // dbg bit 2: per-evaluation stamps instead
+        c.stamps_on = a.stamps != nullptr && !(a.dbg & 20);  // dbg bit 2 / 4: per-evaluation stamps / timeline instead
         c.G = G;
         c.s = s;
         c.epoch = 0;
@@ -2236,10 +2428,11 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
     }
     __syncthreads();
     // optional phase stamps (debug: a.stamps != null): s_memtime deltas on thread 0
-    const bool stamps_on = a.stamps != nullptr && !(a.dbg & 4);
+    const bool stamps_on = kStamps && a.stamps != nullptr && !(a.dbg & 20);
     // debug (FMPNP_DBG bit 2): s_memtime at the start of every evaluation of the team's first
     // problem and after its last, [grid][64] in the stamps buffer
-    unsigned long long *ev_stamps = (a.stamps != nullptr && (a.dbg & 4)) ? a.stamps + (size_t)blockIdx.x * 64 : nullptr;
+    unsigned long long *ev_stamps =
+        (kStamps && a.stamps != nullptr && (a.dbg & 4)) ? a.stamps + (size_t)blockIdx.x * 64 : nullptr;
     if (stamps_on && (tid & 63) == 0) {
         for (int k = 0; k < NSTAMP; ++k) st.stamp_ph[tid >> 6][k] = 0;
         st.stamp_t[tid >> 6] = __builtin_amdgcn_s_memtime();
@@ -2258,6 +2451,10 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
         q.hrec = a.hrec;
         q.hflag = a.hflag;
         q.htag = a.htag;
+        q.tl = (kStamps && a.stamps != nullptr && (a.dbg & 16) && p == team) ? a.stamps + (size_t)blockIdx.x * 8 * 16
+                                                                             : nullptr;
+        q.tl_eval = a.dbg >> 8;
+        q.cur_eval = -1;
         bool first_eval = true;
         if constexpr (!TEAM) q.G = 1;
         q.use_ratio = RATIO ? 1 : 0;
@@ -2270,8 +2467,15 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
             q.loss = FMPNP_GEMAN_MCCLURE;
         q.bilinear = (VAR == VAR_BILINEAR || VAR == VAR_BIL_DIRECT) ? 1 : 0;
         long long ngath = 0;  // texel gathers of this wave for this problem
-        while (!st.done) {
-            if (ev_stamps && tid == 0 && p == team && st.n_evals < 63) ev_stamps[st.n_evals] = __builtin_amdgcn_s_memtime();
+        int k = 0;  // evaluations completed: the next one reads sc[k & 1] and Ret[k & 1]
+        while (true) {
+            {
+                const LMScal &sc = st.sc[k & 1];
+                if (sc.done || sc.nan) break;
+            }
+            if (ev_stamps && tid == 0 && p == team && k < 63) ev_stamps[k] = __builtin_amdgcn_s_memtime();
+            q.cur_ev = q.cur_eval = k;
+            tl_stamp(q, 0);
             q.hfirst = first_eval && q.helpers > 0 && p == team;  // helpers serve each team's first problem
             first_eval = false;
             // project, gather, loss (+ partials)
@@ -2292,35 +2496,53 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
             constexpr bool FLV = VAR == VAR_F_GM || VAR == VAR_F_NEAREST;
             const bool held = !FLV && WPS == WPS_LATENCY && spec_vec1<T>(q);
             SpecHold<T> hold;
-            if (kSpec && q.spec && tid < 64 && q.spec_w0 == 0) {
+            const int wave = tid >> 6;
+            if (kSpec && q.spec && wave == 0 && q.spec_w0 == 0) {
                 if (held) spec0_issue<T>(q, mmax, hold);
                 else spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath);
                 dbg_stamp(q.stamps, 12);  // wave 0's own speculation (before the barrier)
             }
+            tl_stamp(q, 4);
             if (TEAM) team_arrive();
             else __syncthreads();
-            if (tid < 64) {
-                if (!TEAM || team_wait()) {
+            tl_stamp(q, 5);
+            // the tail (lm_tail): one workgroup per problem -- three waves, one role each; a team --
+            // wave 0 after the exchange, every role
+            if (TEAM) {
+                if (wave == 0 && team_wait()) {
                     dbg_stamp(q.stamps, 3);  // slowest wave + exchange
-                    const double tot = combine_final_wave(mmax, TEAM);
+                    const double tot = combine_final_wave(mmax, true);
                     dbg_stamp(q.stamps, 4);
-                    lm_update_wave(tot, q.stamps);
+                    tl_stamp(q, 6);
+                    lm_tail(ROLE_ALL, tot, q, k);
+                    tl_stamp(q, 9);
                 }
-                if (kSpec && q.spec && held && q.spec_w0 == 0) {
-                    if (q.ce - q.cb == 64 * V16<T>::n) spec0_finish<T, true>(q, mmax, hold, ngath);
-                    else spec0_finish<T, false>(q, mmax, hold, ngath);
-                    spec_pass<T, true, false>(q, mmax, ngath, nwaves(), 0);  // wave 0's further blocks: withdrawn
-                }
-            } else if (kSpec && q.spec && (int)(tid >> 6) >= q.spec_w0) {
+            } else if (wave < TAIL_ROLES) {
+                dbg_stamp(q.stamps, 3);
+                const double tot = combine_final_wave(mmax, false);
+                dbg_stamp(q.stamps, 4);
+                tl_stamp(q, 6);
+                lm_tail(wave == 0 ? ROLE_ACC : wave == 1 ? ROLE_REJ : ROLE_BOOK, tot, q, k);
+                tl_stamp(q, 9);
+            }
+            if (wave == 0 && kSpec && q.spec && held && q.spec_w0 == 0) {
+                if (q.ce - q.cb == 64 * V16<T>::n) spec0_finish<T, true>(q, mmax, hold, ngath);
+                else spec0_finish<T, false>(q, mmax, hold, ngath);
+                spec_pass<T, true, false>(q, mmax, ngath, nwaves(), 0);  // wave 0's further blocks: withdrawn
+            }
+            if (kSpec && q.spec && wave >= 1 && wave >= q.spec_w0) {
                 // the other waves gather their blocks' predicted next texels meanwhile
                 spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath, -1, q.spec_cap);
                 dbg_stamp(q.stamps, 4);  // waves >= 1: the speculative gathers
+                tl_stamp(q, 10);
             }
             __syncthreads();
+            tl_stamp(q, 11);
             dbg_stamp(q.stamps, 7);  // pose update + barrier
             if (st.abort_flag) break;
+            ++k;
         }
-        if (ev_stamps && tid == 0 && p == team && st.n_evals < 64) ev_stamps[st.n_evals] = __builtin_amdgcn_s_memtime();
+        if (ev_stamps && tid == 0 && p == team && k < 64) ev_stamps[k] = __builtin_amdgcn_s_memtime();
         // texel gathers of the problem: a team's members add their waves' counts to the zeroed
         // result (G > 1); one workgroup sums its waves' counts in LDS and stores the total with
         // the other result fields (G = 1: the launch needs no memset)
@@ -2332,7 +2554,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
             if ((tid & 63) == 0) st.wg_gath[tid >> 6] = ngath;
             __syncthreads();
         }
-        problem_end(!TEAM);
+        problem_end(!TEAM, k, q.tl);
     }
     if (stamps_on && (tid & 63) == 0)
         for (int k = 0; k < NSTAMP; ++k)
