@@ -16,7 +16,7 @@ Default: weak scaling, --batch 128 queries per GPU (configs[2]'s 1024 queries at
 
 Roofline (dominant kernel = the LM launch): `achieved` = HBM bytes per launch from the
 committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this exact workload
-(profiles/r02_pmc_<tag>.json, tools/gpu_profile_r02.sh; FETCH_SIZE doubled per
+(profiles/rNN_pmc_<tag>.json of the newest round, tools/gpu_profile.sh; FETCH_SIZE doubled per
 MI355X_MICROARCH.md) ÷ the launch time measured here with HIP events; without a matching
 profile, the bytes the kernel's gathers move (counted live: texel gathers x 16C + the
 fp64 points).  SURVEY.md §8d's reference-equivalent figure (every point re-read every
@@ -106,7 +106,7 @@ def spawn_ranks(n):
 
 
 def workload_tag(B, init, ratio, memo, sampling, layout, spec=True):
-    """Key of a workload in profiles/r02_pmc_<tag>.json."""
+    """Key of a workload in profiles/rNN_pmc_<tag>.json."""
     t = f"b{B}_{init}"
     if ratio is not None:
         t += f"_ratio{ratio:g}"
@@ -124,13 +124,16 @@ def workload_tag(B, init, ratio, memo, sampling, layout, spec=True):
 def load_traffic(tag):
     """(HBM bytes per launch, kernel name, rocprof avg ns) of a workload from its committed
     rocprofv3 PMC summary, or (None, None, None)."""
-    try:
-        with open(os.path.join(ROOT, "profiles", f"r02_pmc_{tag}.json")) as f:
-            d = json.load(f)
+    for rnd in ("r03", "r02"):  # the newest round's profile of the workload
+        path = os.path.join("profiles", f"{rnd}_pmc_{tag}.json")
+        try:
+            with open(os.path.join(ROOT, path)) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
         name = (d.get("kernel") or "").replace("void ", "").replace("(fmpnp::LaunchArgs)", "")
-        return d.get("hbm_bytes_per_launch"), name or None, d.get("kernel_avg_ns")
-    except (OSError, ValueError):
-        return None, None, None
+        return d.get("hbm_bytes_per_launch"), name or None, d.get("kernel_avg_ns"), path
+    return None, None, None, None
 
 
 def gather_bytes_rule(sampling, layout):
@@ -147,12 +150,12 @@ def roofline(tag, res, kernel_s, B, sampling, layout):
     gathers = int(sum(r["texel_gathers"] for r in res))
     n_evals = int(sum(r["n_evals"] for r in res))
     gathered = gathers * per_gather + B * N_PTS * 24
-    traffic, kname, prof_ns = load_traffic(tag)
+    traffic, kname, prof_ns, prof_path = load_traffic(tag)
     ach_bytes = traffic if traffic else gathered
     ach = ach_bytes / kernel_s
     return {"bound": "hbm", "achieved": round(ach / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK, 4), "traffic": traffic,
-            "achieved_source": ("rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r02_pmc_%s.json" % tag) if traffic
+            "achieved_source": ("rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, %s" % prof_path) if traffic
             else "texel gathers counted by the kernel x bytes per gather (no matching PMC profile)",
             "kernel": kname or "fmpnp::lm_kernel", "avg_kernel_ms": round(kernel_s * 1e3, 4),
             "rocprof_avg_kernel_ms": round(prof_ns / 1e6, 4) if prof_ns else None,
@@ -367,21 +370,13 @@ def run_legs(args, dev, probs, feats, inputs, opts, res_main, rf, _lib, synth):
         ms, r = time_launches(rf.AsyncBatch(probs, opt(speculate=False)), 10, stream)
         out["no_spec"] = leg_summary(workload_tag(B, args.init, args.ratio, memo, args.sampling, args.layout, False),
                                      ms, r, B, args.sampling, args.layout, base=res_main)
-    if "no_memo" in args.legs and memo:  # the reference's data movement: every texel re-read
-        ms, r = time_launches(rf.AsyncBatch(probs, opt(memoize=False)), 5, stream)
-        out["no_memo"] = leg_summary(workload_tag(B, args.init, args.ratio, False, args.sampling, args.layout), ms,
-                                     r, B, args.sampling, args.layout, base=res_main)
     if "bilinear" in args.legs and args.sampling == "nearest" and args.layout == "fgrad":  # extension
-        # the cell memo (default), and every supported point sampled at every evaluation
+        # the cell memo (default); direct sampling of every point at every evaluation runs in the
+        # 1024-query leg below (an HBM-streamed working set)
         ms, r = time_launches(rf.AsyncBatch(probs, opt(sampling="bilinear")), 10, stream)
         out["bilinear"] = leg_summary(workload_tag(B, args.init, args.ratio, memo, "bilinear", "fgrad"), ms, r, B,
                                       "bilinear", "fgrad")
         out["bilinear"]["launch"] = _lib.last_launch()
-        ms, r2 = time_launches(rf.AsyncBatch(probs, opt(sampling="bilinear", memoize=False)), 3, stream)
-        out["bilinear_direct"] = leg_summary(workload_tag(B, args.init, args.ratio, False, "bilinear", "fgrad"), ms,
-                                             r2, B, "bilinear", "fgrad")
-        out["bilinear_direct"]["max_rot_diff_vs_memo_rad"] = float(max(rot_angle(a["R"], b["R"])
-                                                                       for a, b in zip(r, r2)))
     if "layout_f" in args.legs and args.layout == "fgrad" and args.sampling == "nearest":
         fp = []
         for q, inp in enumerate(inputs):
@@ -400,17 +395,24 @@ def run_legs(args, dev, probs, feats, inputs, opts, res_main, rf, _lib, synth):
         out["end_to_end"] = pipeline_leg(dev, synth)
     if "pyramid1664" in args.legs:
         out["pyramid_robotcar_1664"] = pyramid_leg(dev, rf, synth, _lib, stream)
-    if "fixed1024" in args.legs and B < 1024 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
-        out["fixed_total_1024"] = fixed_total_leg(args, dev, probs, feats, inputs, opts, rf, synth, stream)
+    if ({"fixed1024", "no_memo", "bilinear"} & args.legs) and B < 1024 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        out.update(fixed_total_leg(args, dev, probs, feats, inputs, opts, rf, synth, stream, opt))
     if "cpu" in args.legs and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         out["cpu_baseline"] = cpu_baseline(args, res_main, synth, dev)
     return out
 
 
-def fixed_total_leg(args, dev, probs, feats, inputs, opts, rf, synth, stream):
-    """SURVEY.md §8e's fixed total of 1024 queries on ONE GPU (the N=1 point of the strong-scaling
-    curve): the headline's queries plus the next ones by global index, one launch.  Packed
-    layout when it fits in HBM (1024 x 236 MB), else the f-only layout."""
+def fixed_total_leg(args, dev, probs, feats, inputs, opts, rf, synth, stream, opt):
+    """The 1024-query set resident on ONE GPU (the headline's queries plus the next ones by global
+    index; packed layout when it fits in HBM, 1024 x 236 MB, else the f-only layout):
+      fixed_total_1024   SURVEY.md §8e's fixed total of 1024 on one GPU (the N = 1 point of the
+                         strong-scaling curve), memoised, one launch;
+      no_memo            every point's texel re-read at every evaluation (the reference's data
+                         movement), the same 1024 queries;
+      bilinear_direct    bilinear sampling of every supported point at every evaluation.
+    The last two stream a working set of >= 2 GB per launch, far beyond the 256 MB Infinity Cache,
+    so their traffic is HBM traffic (at B = 128 their per-launch working set is about the cache's
+    size and part of it was served from there)."""
     from fmpnp import _lib
     n = 1024
     torch.cuda.synchronize()
@@ -426,15 +428,33 @@ def fixed_total_leg(args, dev, probs, feats, inputs, opts, rf, synth, stream):
         ps.append(rf.make_problem(f, inp["fref"], inp["pts3d"], inp["K"], inp["im_width"], inp["im_height"],
                                   inp["R0"], inp["t0"]))
         del inp
+    out = {}
+    memo = not args.no_memo
     # (226 GB of freshly allocated maps: the first launches also warm the address translation)
     ms, r = time_launches(rf.AsyncBatch(ps, opts), 20, stream, warmup=3)
-    d = leg_summary(workload_tag(n, args.init, args.ratio, not args.no_memo, args.sampling, layout), ms, r, n,
-                    args.sampling, layout)
-    d.update(layout=layout, launch=_lib.last_launch(),
-             resident_GiB=round(torch.cuda.memory_allocated(dev) / 2**30, 1))
+    if "fixed1024" in args.legs:
+        d = leg_summary(workload_tag(n, args.init, args.ratio, memo, args.sampling, layout), ms, r, n,
+                        args.sampling, layout)
+        d.update(layout=layout, launch=_lib.last_launch(),
+                 resident_GiB=round(torch.cuda.memory_allocated(dev) / 2**30, 1))
+        out["fixed_total_1024"] = d
+    note = ("1024 queries resident: >= 2 GB of distinct texels per launch, beyond the 256 MB Infinity Cache "
+            "(HBM-streamed)")
+    if "no_memo" in args.legs and memo and layout == "fgrad":
+        ms2, r2 = time_launches(rf.AsyncBatch(ps, opt(memoize=False)), 3, stream)
+        d = leg_summary(workload_tag(n, args.init, args.ratio, False, args.sampling, layout), ms2, r2, n,
+                        args.sampling, layout, base=r)
+        d.update(launch=_lib.last_launch(), working_set=note)
+        out["no_memo"] = d
+    if "bilinear" in args.legs and args.sampling == "nearest" and layout == "fgrad":
+        ms3, r3 = time_launches(rf.AsyncBatch(ps, opt(sampling="bilinear", memoize=False)), 2, stream)
+        d = leg_summary(workload_tag(n, args.init, args.ratio, False, "bilinear", "fgrad"), ms3, r3, n, "bilinear",
+                        "fgrad")
+        d.update(launch=_lib.last_launch(), working_set=note)
+        out["bilinear_direct"] = d
     del ps
     torch.cuda.empty_cache()
-    return d
+    return out
 
 
 def pyramid_leg(dev, rf, synth, _lib, stream, B=32):

@@ -420,7 +420,7 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
         // more than fit in it would delay the evaluation's closing barrier)
         // (read per launch: measurement and test knobs, FMPNP_SPEC_CAP / FMPNP_SPEC_W0)
         const char *ec = getenv("FMPNP_SPEC_CAP"), *ew = getenv("FMPNP_SPEC_W0");
-        a.spec_cap = ec ? std::max(0, atoi(ec)) : 4;
+        a.spec_cap = ec ? std::max(0, atoi(ec)) : 2;
         a.spec_w0 = ew ? std::max(0, atoi(ew)) : 4;
     }
     {

@@ -82,6 +82,7 @@ struct Ctx {
     const double *pts;
     double K[9];
     int p, N, Hf, Wf, cs, cb, ce, ld_ref, im_w, im_h, vec;
+    float txpx, typx, pxtx, pypx;  // texels per image pixel, image pixels per texel (x, y)
     UDiv div_h, div_w;    // exact floor division by im_h, im_w (indexing_)
     int p0, M, c0, LC, NC;
 };
@@ -108,7 +109,6 @@ struct PC {
     const unsigned long long *hflag;
     unsigned long long htag;
     int dbg;
-    float txpx, typx, pxtx, pypx;  // texels per image pixel and image pixels per texel (x, y)
     int sob_norm, sob_rep;  // FMPNP_LAYOUT_F: the in-gather Sobel's flags
     double alpha;
     double *part_g;       // this team's partial slots [2][nc_max][NV] (G > 1)
@@ -147,9 +147,12 @@ __device__ __forceinline__ P *ufirst(P *p) {
 // the state before the evaluation while one of them writes the next.
 struct LMScal {
     double lambda, lr, prev, best, initial;
-    int best_inl, n_evals, n_steps, n_accepted, status, done, has_best, ret_current;
+    int done;
     int nan;                // a step came out NaN (model.py:411-413): written by the stepping wave only
+    int best_inl, n_evals, n_steps, n_accepted, status, has_best, ret_current;
 };
+static_assert(offsetof(LMScal, nan) == offsetof(LMScal, done) + 4 && offsetof(LMScal, done) % 8 == 0,
+              "done / nan: one 8-byte read at the top of every evaluation");
 constexpr int TAIL_ROLES = 3;  // tail waves of the split tail: accept stepper, reject stepper, bookkeeper
 struct LMState {
     double tot[TAIL_ROLES][NV];  // each tail wave's combined totals of the evaluation (broadcast operands)
@@ -193,10 +196,6 @@ __device__ __forceinline__ PC load_pc() {
     q.spec_cap = ufirst(c.spec_cap);
     q.spec_w0 = ufirst(c.spec_w0);
     q.dbg = ufirst(c.dbg);
-    q.txpx = (float)q.Wf / (float)q.im_w;
-    q.typx = (float)q.Hf / (float)q.im_h;
-    q.pxtx = (float)q.im_w / (float)q.Wf;
-    q.pypx = (float)q.im_h / (float)q.Hf;
     q.bilinear = ufirst(c.sampling == FMPNP_BILINEAR ? 1 : 0);
     q.use_ratio = ufirst(c.use_ratio);
     q.alpha = ufirst(c.alpha);
@@ -235,8 +234,28 @@ __device__ __forceinline__ bool project_pc(const PC &q, const double P[3], int &
 #pragma clang fp contract(off)
         const double u0 = q.fx * P[0] + q.cx * P[2];
         const double u1 = q.fy * P[1] + q.cy * P[2];
-        qx = u0 / P[2];
-        qy = u1 / P[2];
+        if (q.bilinear) {  // the taps use the unrounded quotients: the reference's exact division
+            qx = u0 / P[2];
+            qy = u1 / P[2];
+        } else {
+            // Only the rounded pixel matters here: the quotients by one refined reciprocal (within
+            // ~3 ulp of the correctly rounded u / z) round to the same integers as the IEEE
+            // quotients unless one lies within 8 ulp of a half-integer (rint's boundary, ties to
+            // even) -- those lanes, and any z outside [2^-1000, 2^1000] or a non-finite quotient,
+            // take the exact divisions.  So px, py and the support test are the reference's; qx, qy
+            // only feed the speculation's next-texel prediction.
+            const double z = P[2], r = recip(z);
+            double ax = u0 * r, ay = u1 * r;
+            const double ex = fabs(fabs(ax - rint(ax)) - 0.5), ey = fabs(fabs(ay - rint(ay)) - 0.5);
+            const bool fast = fabs(z) > 0x1p-1000 && fabs(z) < 0x1p+1000 && ex > fabs(ax) * 0x1p-49 &&
+                              ey > fabs(ay) * 0x1p-49;  // (false for NaN / infinite quotients)
+            if (!fast) {
+                ax = u0 / z;
+                ay = u1 / z;
+            }
+            qx = ax;
+            qy = ay;
+        }
         const double px = rint(qx) - 1.0, py = rint(qy) - 1.0;
         if (!(px >= 0.0 && px < (double)q.im_w && py >= 0.0 && py < (double)q.im_h)) return false;
         x = (int)px;
@@ -416,6 +435,10 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
         for (int k = 0; k < 9; ++k) c.K[k] = pb->K[k];
         c.div_h = udiv_make((unsigned)c.im_h);
         c.div_w = udiv_make((unsigned)c.im_w);
+        c.txpx = (float)c.Wf / (float)c.im_w;
+        c.typx = (float)c.Hf / (float)c.im_h;
+        c.pxtx = (float)c.im_w / (float)c.Wf;
+        c.pypx = (float)c.im_h / (float)c.Hf;
         c.NC = (c.N + CH - 1) / CH;
         c.c0 = (int)(((long)c.NC * c.s) / c.G);
         const int c1 = (int)(((long)c.NC * (c.s + 1)) / c.G);
@@ -1443,9 +1466,10 @@ __device__ __forceinline__ int spec_target(const PC &q, double qx, double qy, in
     const float mx = fabsf(fx - *qpx), my = fabsf(fy - *qpy);  // NaN before the first motion: none
     *qpx = fx;
     *qpy = fy;
-    const float sx = (fx - 0.5f) * q.txpx, sy = (fy - 0.5f) * q.typx;  // continuous texel coordinates
+    const Ctx &c = reinterpret_cast<const LMState *>(lm_lds)->c;  // (broadcast reads: not held in registers)
+    const float sx = (fx - 0.5f) * c.txpx, sy = (fy - 0.5f) * c.typx;  // continuous texel coordinates
     const float ax = sx - floorf(sx), ay = sy - floorf(sy);
-    const bool cx = fminf(ax, 1.0f - ax) * q.pxtx < mx, cy = fminf(ay, 1.0f - ay) * q.pypx < my;
+    const bool cx = fminf(ax, 1.0f - ax) * c.pxtx < mx, cy = fminf(ay, 1.0f - ay) * c.pypx < my;
     const int c2 = col + (cx ? (ax < 0.5f ? -1 : 1) : 0), r2 = row + (cy ? (ay < 0.5f ? -1 : 1) : 0);
     return ((cx || cy) && c2 >= 0 && c2 < q.Wf && r2 >= 0 && r2 < q.Hf) ? r2 * q.Wf + c2 : -1;
 }
@@ -1496,102 +1520,6 @@ __device__ __forceinline__ void spec_pass(const PC &q, int mmax, long long &ngat
     }
 }
 
-// The packed layout's one-round-trip gather applies (16-byte loads, every channel of the
-// slice within a lane's two rounds): the pooled speculation's precondition.
-template <typename T>
-__device__ __forceinline__ bool spec_vec1(const PC &q) {
-    constexpr int V = V16<T>::n;
-    return ((((uintptr_t)q.feat) | ((uintptr_t)q.fref)) & 15) == 0 && q.cs % V == 0 && q.ld % V == 0 &&
-           q.cb % V == 0 && (q.ce - q.cb) % V == 0 && q.ce - q.cb <= 64 * V;
-}
-
-// Wave 0's speculation (the packed layout with every channel in one round trip, i.e. the
-// headline path): wave 0 runs the LM tail between the two barriers, so it only ISSUES the
-// loads of (one pair of) its first block's predicted texels before the first barrier
-// and reduces them after the tail -- the memory round trip hides behind the barrier wait
-// and the tail instead of delaying either.  Further predicted points (rare) and further
-// blocks go through the ordinary pipeline after the tail.  Same loads and arithmetic as
-// every other gather: identical records.
-struct SpecPt {
-    int j;     // lane of the point in block 0 (-1: none)
-    int o;     // predicted texel
-    bool s;    // current slot is rec2 (the gather fills rec)
-};
-template <typename T>
-struct SpecHold {
-    GLoad<T> A;
-    SpecPt a0, a1;
-    unsigned long long rest;  // block 0's remaining wanted points
-    bool any;
-};
-
-template <typename T>
-__device__ __forceinline__ void spec0_issue(const PC &q, int mmax, SpecHold<T> &h) {
-    constexpr int V = V16<T>::n;
-    const int lane = threadIdx.x & 63, l32 = lane & 31;
-    const bool hi = lane >= 32;
-    const int *tex = lds_tex(mmax, true), *spec = lds_spec(mmax, true), *slot = lds_slot(mmax, true);
-    const int *tex2 = lds_tex2(mmax, true);
-    const bool valid = lane < q.M;
-    const int sp = valid ? spec[lane] : -1, sl = slot[lane];
-    unsigned long long m = __ballot(valid && sp >= 0 && sp != tex[lane] && sp != tex2[lane]);
-    auto take = [&]() -> SpecPt {
-        if (!m) return SpecPt{-1, 0, false};
-        const int j = __builtin_ctzll(m);
-        m &= m - 1;
-        return SpecPt{j, __builtin_amdgcn_readlane(sp, j), __builtin_amdgcn_readlane(sl, j) != 0};
-    };
-    h.a0 = take();
-    h.a1 = take();
-    // the held pair only: wave 0 gathers nothing else after its tail (further predictions of
-    // its block are withdrawn; the next evaluation gathers those points on demand)
-    if (valid && (m >> lane) & 1ull) lds_spec(mmax, true)[lane] = -1;
-    h.rest = 0;
-    h.any = h.a0.j >= 0;
-    if (!h.any) return;
-    const T *feat = reinterpret_cast<const T *>(q.feat);
-    const T *fref = reinterpret_cast<const T *>(q.fref);
-    const int gc = q.cb + l32 * V;
-    const bool has1 = gc < q.ce, has2 = gc + 32 * V < q.ce;
-    const int gc1 = has1 ? gc : q.cb, gc2 = has2 ? gc + 32 * V : gc1;
-    auto issue = [&](GLoad<T> &g, const SpecPt &lo, const SpecPt &hp) {  // no second point: re-read the first
-        const SpecPt &p = hi && hp.j >= 0 ? hp : lo;
-        g_issue<T>(g, feat + (size_t)p.o * 3 * q.cs, fref + (size_t)(q.p0 + p.j) * q.ld, q.cs, gc1, gc2);
-    };
-    issue(h.A, h.a0, h.a1);
-}
-
-template <typename T, bool FULL>
-__device__ __forceinline__ void spec0_finish(const PC &q, int mmax, SpecHold<T> &h, long long &ngath) {
-    constexpr int V = V16<T>::n;
-    const int lane = threadIdx.x & 63, l32 = lane & 31;
-    const bool hi = lane >= 32;
-    double *rec = lds_rec(mmax), *rec2 = lds_rec2(mmax);
-    const int rs = lds_rs(mmax);
-    const int gc = q.cb + l32 * V;
-    const bool has1 = gc < q.ce, has2 = gc + 32 * V < q.ce;
-    const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
-    const bool wlane = (lane & 3) == 0 && e6 < 6;
-    auto consume = [&](const GLoad<T> &g, const SpecPt &lo, const SpecPt &hp) {
-        double v[8];
-        g_consume<T, FULL>(g, has1, has2, v);
-        const double r = reduce8_in32(v, lane);
-        const SpecPt &p = hi ? hp : lo;
-        if (wlane && p.j >= 0) (p.s ? rec : rec2)[(size_t)e6 * rs + p.j] = r;  // the idle slot
-        ngath += hp.j >= 0 ? 2 : 1;
-    };
-    if (h.any) consume(h.A, h.a0, h.a1);
-    if (h.rest) {  // block 0's points beyond the held pair
-        const int *spec = lds_spec(mmax, true), *slot = lds_slot(mmax, true);
-        const bool valid = lane < q.M;
-        const int sp = valid ? spec[lane] : -1;
-        const size_t fo = (size_t)(wlane ? e6 : 0) * rs;
-        const RecDst rd{rec + fo, rec2 + fo, __ballot(valid && slot[lane] != 0)};
-        gather_records<T, true, false>(q, h.rest, sp, 0, 0, rd, wlane);
-        ngath += __popcll(h.rest);
-    }
-}
-
 // ---------------------------------------------------------------------------
 // One evaluation at (Re, te) over the wave's blocks (no workgroup barrier inside).
 // Without the ratio test each block goes straight on to its chunk partials; with it the
@@ -1600,7 +1528,7 @@ __device__ __forceinline__ void spec0_finish(const PC &q, int mmax, SpecHold<T> 
 // SP: the variant can speculate (nearest sampling; bilinear never memoises).
 // ---------------------------------------------------------------------------
 template <typename T, bool PIPE, bool FL, bool SP, bool HELP>
-__device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ngath) {
+__device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ngath, const double pose[12]) {
     LMState &st = S();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool hi = lane >= 32;
@@ -1622,14 +1550,13 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
     double *rec2 = lds_rec2(mmax);
     double *dst_g = q.part_g;
     if (q.G > 1) dst_g += (size_t)((ufirst((int)st.c.epoch) + 1) & 1) * q.nc_max * NV;
-    // the pose evaluated: one LDS broadcast read per evaluation, kept in VGPRs (moving it to
-    // SGPRs costs 24 v_readfirstlane and SGPR spills)
+    // the pose evaluated (read by the caller with the loop's state, one LDS burst; kept in VGPRs:
+    // moving it to SGPRs costs 24 v_readfirstlane and SGPR spills)
     double Re[9], te[3];
-    const double *pev = st.Ret[q.cur_ev & 1];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Re[k] = pev[k];
+    for (int k = 0; k < 9; ++k) Re[k] = pose[k];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) te[k] = pev[9 + k];
+    for (int k = 0; k < 3; ++k) te[k] = pose[9 + k];
     double lmax = -1.0;  // -1: nothing supported seen yet
     for (int blk = wave; blk * 64 < M; blk += nwaves()) {
         const int i = blk * 64 + lane;
@@ -1641,23 +1568,31 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         double Pc[3] = {0.0, 0.0, 1.0};
         int off = -1, rc = 0, pred = -1;
         Taps tp;
-        // the point's memo state, read before the projection (it does not depend on the pose)
+        // the point's coordinates and memo state in one burst of LDS reads (clamped index, no
+        // per-lane branch: a single round trip before the projection; none depends on the pose)
         const int ii = valid ? i : 0;
-        const int old = valid ? tex[ii] : -1;
-        int t2 = -1, sl = 0;
+        const double X0 = X[ii], X1 = X[rs + ii], X2 = X[2 * rs + ii];
+        const int old_r = tex[ii];
+        int t2 = -1, sl = 0, sp = -1;
         float qpx = 0.0f, qpy = 0.0f;
-        if (spec_on) {
+        if (SP) {  // (the speculating variants' arrays; unused below spec_w0)
             t2 = tex2[ii];
             sl = slot[ii];
             qpx = qp[ii];
             qpy = qp[mmax + ii];
+            sp = spec[ii];
+        }
+        const int old = valid ? old_r : -1;
+        if (spec_on) {
             // the last spec pass filled the idle slot with the predicted texel when it was
             // neither slot's (spec_pass / spec_pooled apply this same test)
-            const int sp = spec[ii];
             if (sp >= 0 && sp != old && sp != t2) t2 = sp;
+        } else {
+            t2 = -1;
+            sl = 0;
         }
         if (valid) {
-            transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
+            transform_pt(Re, te, X0, X1, X2, Pc);
             int x, y;
             double qx, qy;
             if (project_pc(q, Pc, x, y, qx, qy)) {
@@ -1904,14 +1839,14 @@ __device__ __forceinline__ void contrib_pass(const PC &q, int mmax) {
 // h, h+2, h+4, ... in order; the halves are then added.  Depends only on the chunk
 // partials and NC -- not on G, placement or timing.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double combine_final_wave(int mmax, bool team) {
+__device__ __forceinline__ double combine_final_wave(int mmax, bool team, bool spec) {
     LMState &st = S();
     const Ctx &c = st.c;
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
     const int NC = c.NC;
     double t = 0.0;
     if (!team) {
-        const double *src = lds_part(mmax, c.spec);
+        const double *src = lds_part(mmax, spec);
         double v[4];
         for (int r0 = h; r0 < NC; r0 += 8) {  // four loads in flight, adds in chunk order
 #pragma unroll
@@ -2443,6 +2378,9 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
         if constexpr (kHelp) helper_run<T>(a, mmax);
         return;
     }
+#if defined(FMPNP_PRIO) && FMPNP_PRIO
+    if ((tid >> 6) >= 4) __builtin_amdgcn_s_setprio(1);  // experiment: the younger half first
+#endif
     for (int p = team; p < a.n; p += a.teams) {
         problem_begin(a.probs + p, p, mmax);
         PC q = load_pc();
@@ -2456,12 +2394,19 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
         q.tl_eval = a.dbg >> 8;
         q.cur_eval = -1;
         bool first_eval = true;
-        if constexpr (!TEAM) q.G = 1;
+        if constexpr (!TEAM) {  // one workgroup: it owns every chunk (compile-time constants)
+            q.G = 1;
+            q.c0 = 0;
+            q.p0 = 0;
+        }
         q.use_ratio = RATIO ? 1 : 0;
-        // speculation: the nearest-sampling variants of the latency build
+        // speculation: the nearest-sampling variants of the latency build.  The planner runs a
+        // _SPEC variant exactly when it enables speculation (memoised), so the flag is a constant
         constexpr bool kSpec = kSpecBuild && WPS == WPS_LATENCY &&
                                (VAR == VAR_GM_SPEC || VAR == VAR_NEAREST_SPEC || VAR == VAR_GM_SPEC_H ||
                                 VAR == VAR_NEAREST_SPEC_H);
+        q.spec = kSpec ? 1 : 0;
+        if constexpr (kSpec) q.no_memo = 0;
         if constexpr (VAR == VAR_GM || VAR == VAR_F_GM || VAR == VAR_GM_SPEC || VAR == VAR_GM_SPEC_H ||
                       VAR == VAR_GM_H)
             q.loss = FMPNP_GEMAN_MCCLURE;
@@ -2469,9 +2414,14 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
         long long ngath = 0;  // texel gathers of this wave for this problem
         int k = 0;  // evaluations completed: the next one reads sc[k & 1] and Ret[k & 1]
         while (true) {
+            // the loop's state and the pose to evaluate, read together (one LDS round trip)
+            double pose[12];
             {
-                const LMScal &sc = st.sc[k & 1];
-                if (sc.done || sc.nan) break;
+                const double *pev = st.Ret[k & 1];
+#pragma unroll
+                for (int j = 0; j < 12; ++j) pose[j] = pev[j];
+                const int2 dn = *reinterpret_cast<const int2 *>(&st.sc[k & 1].done);
+                if ((dn.x | dn.y) != 0) break;
             }
             if (ev_stamps && tid == 0 && p == team && k < 63) ev_stamps[k] = __builtin_amdgcn_s_memtime();
             q.cur_ev = q.cur_eval = k;
@@ -2485,23 +2435,14 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
             if constexpr (VAR == VAR_BILINEAR)
                 lmax = eval_pass_bil<T>(q, mmax, ngath);
             else
-                lmax = eval_pass<T, true, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST), kSpec, kHelp>(q, mmax, ngath);
+                lmax = eval_pass<T, true, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST), kSpec, kHelp>(q, mmax, ngath,
+                                                                                                   pose);
             if (q.use_ratio) {
                 if (!ratio_exchange(lmax)) break;
                 contrib_pass(q, mmax);
             }
-            // speculation: every wave for its own blocks -- wave 0 issues the loads of its first
-            // block's predictions now and reduces them after the tail when the packed one-round-
-            // trip gather applies (held), else it speculates entirely before the barrier
-            constexpr bool FLV = VAR == VAR_F_GM || VAR == VAR_F_NEAREST;
-            const bool held = !FLV && WPS == WPS_LATENCY && spec_vec1<T>(q);
-            SpecHold<T> hold;
             const int wave = tid >> 6;
-            if (kSpec && q.spec && wave == 0 && q.spec_w0 == 0) {
-                if (held) spec0_issue<T>(q, mmax, hold);
-                else spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath);
-                dbg_stamp(q.stamps, 12);  // wave 0's own speculation (before the barrier)
-            }
+            constexpr bool FLV = VAR == VAR_F_GM || VAR == VAR_F_NEAREST;
             tl_stamp(q, 4);
             if (TEAM) team_arrive();
             else __syncthreads();
@@ -2511,7 +2452,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
             if (TEAM) {
                 if (wave == 0 && team_wait()) {
                     dbg_stamp(q.stamps, 3);  // slowest wave + exchange
-                    const double tot = combine_final_wave(mmax, true);
+                    const double tot = combine_final_wave(mmax, true, kSpec);
                     dbg_stamp(q.stamps, 4);
                     tl_stamp(q, 6);
                     lm_tail(ROLE_ALL, tot, q, k);
@@ -2519,21 +2460,22 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
                 }
             } else if (wave < TAIL_ROLES) {
                 dbg_stamp(q.stamps, 3);
-                const double tot = combine_final_wave(mmax, false);
+                const double tot = combine_final_wave(mmax, false, kSpec);
                 dbg_stamp(q.stamps, 4);
                 tl_stamp(q, 6);
                 lm_tail(wave == 0 ? ROLE_ACC : wave == 1 ? ROLE_REJ : ROLE_BOOK, tot, q, k);
                 tl_stamp(q, 9);
             }
-            if (wave == 0 && kSpec && q.spec && held && q.spec_w0 == 0) {
-                if (q.ce - q.cb == 64 * V16<T>::n) spec0_finish<T, true>(q, mmax, hold, ngath);
-                else spec0_finish<T, false>(q, mmax, hold, ngath);
-                spec_pass<T, true, false>(q, mmax, ngath, nwaves(), 0);  // wave 0's further blocks: withdrawn
-            }
-            if (kSpec && q.spec && wave >= 1 && wave >= q.spec_w0) {
-                // the other waves gather their blocks' predicted next texels meanwhile
-                spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath, -1, q.spec_cap);
-                dbg_stamp(q.stamps, 4);  // waves >= 1: the speculative gathers
+            // speculative gathers of the predicted next texels (spec_pass), while wave 0 finishes the
+            // tail: each wave >= 1 for its own blocks (waves 1 and 2 after their tail roles), and wave
+            // 3 -- idle in the tail -- for wave 0's blocks too.  Their channel sums then leave the next
+            // evaluation's point phase, which issue-bounds the SIMDs.
+            if (kSpec && q.spec) {
+                if (wave >= 1 && wave >= q.spec_w0) {
+                    spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath, -1, q.spec_cap);
+                    dbg_stamp(q.stamps, 4);  // the speculative gathers
+                }
+                if (wave == 3 && q.spec_w0 == 0) spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath, 0, q.spec_cap);
                 tl_stamp(q, 10);
             }
             __syncthreads();
