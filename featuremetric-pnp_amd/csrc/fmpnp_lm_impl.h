@@ -2230,11 +2230,14 @@ __device__ __forceinline__ void lm_tail(int role, double tot, const PC &q, int k
     for (int j = 0; j < 21; ++j) Hu[j] = hs[j];
 #pragma unroll
     for (int j = 0; j < 6; ++j) gv[j] = hs[21 + j];
+    tl_stamp(q, 12);  // (stamps build: the operands have arrived)
     const bool solved = ldlt_step(Hu, gv, lam, lr, delta);
     // (the step is formed here, not sunk past the decision's branch: the decision's instructions
     // then fill the solve's dependency stalls instead of adding to them)
     asm volatile("" ::"v"(delta[0]), "v"(delta[1]), "v"(delta[2]), "v"(delta[3]), "v"(delta[4]), "v"(delta[5]));
+    tl_stamp(q, 13);
     const Decision d = lm_decide(tot, sv, mode, n_iters);
+    tl_stamp(q, 14);
     if (d.stop || d.take != acc) return;
     tl_stamp(q, 8);
     lm_step_store(hs, delta, solved, lam, lr, base, nxt);

@@ -13,7 +13,7 @@ import numpy as np, torch
 from fmpnp import _lib, refine as rf, synth
 
 SITES = ["start", "projected", "gathered", "contrib", "pre-barrier", "barrier1", "combined", "bookkeeping",
-         "solved", "pose stored", "spec done", "barrier2"]
+         "solved", "pose stored", "spec done", "barrier2", "acc operands", "acc ldlt", "acc decided"]
 dev = torch.device("cuda", 0)
 probs = []
 for q in range(B):
@@ -42,4 +42,13 @@ m = np.nanmean(rel, 0)
 print(f"B={B} eval {E} ({init}), {len(t)} workgroups, cycles since wave 0's start (mean over WGs)")
 print("site".ljust(13) + "".join(f"   w{w:d}  " for w in range(8)))
 for k, name in enumerate(SITES):
+    if np.all(np.isnan(m[:, k])):
+        continue
     print(name.ljust(13) + "".join("   ----  " if np.isnan(m[w, k]) else f"{m[w, k]:7.0f}  " for w in range(8)))
+# the slowest wave of each workgroup sets its barrier: mean over workgroups of the per-WG maximum
+for k in (3, 4, 10):
+    v = rel[:, :, k]
+    if np.all(np.isnan(v)):
+        continue
+    print(f"{SITES[k]:13s} per-WG max over waves: mean {np.nanmean(np.nanmax(v, 1)):7.0f}; "
+          f"argmax wave histogram {np.bincount(np.nanargmax(np.where(np.isnan(v), -1e18, v), 1), minlength=8).tolist()}")
