@@ -253,29 +253,52 @@ __host__ __device__ __forceinline__ double kc(double v) {
 #endif
     return v;
 }
+// The same constant materialised by two s_mov_b32 of its halves inside volatile asm, so it can
+// be neither hoisted out of the loop nor kept live (and spilled to VGPR lanes) between uses:
+// kc() pins the use site, but the compiler may still hoist the constant's s_mov pair out of the
+// problem loop and spill the SGPR pair, which costs v_readlane reloads on the LM tail.
+template <unsigned long long B>
+__host__ __device__ __forceinline__ double kcb() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    unsigned lo, hi;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "i"((int)(unsigned)(B & 0xffffffffull)));
+    asm volatile("s_mov_b32 %0, %1" : "=s"(hi) : "i"((int)(unsigned)(B >> 32)));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+#else
+    return __builtin_bit_cast(double, B);
+#endif
+}
+#ifndef FMPNP_KC_ASM
+#define FMPNP_KC_ASM 1
+#endif
+#if FMPNP_KC_ASM
+#define KC(x) ::fmpnp::kcb<__builtin_bit_cast(unsigned long long, (double)(x))>()
+#else
+#define KC(x) ::fmpnp::kc(x)
+#endif
 
 // sin, cos of 0 <= x <= pi/4 by Horner-form Taylor series to x^17 / x^18 (truncation
 // below 1e-19 relative; a few ulp of rounding): ~20 register-resident fp64 operations
 // instead of the library's range-reduced sincos on the LM tail's critical path.
 __host__ __device__ __forceinline__ void sincos_small(double x, double &s, double &c) {
     const double z = x * x;
-    double ps = kc(1.0 / 355687428096000.0);
-    ps = fma(ps, z, kc(-1.0 / 1307674368000.0));
-    ps = fma(ps, z, kc(1.0 / 6227020800.0));
-    ps = fma(ps, z, kc(-1.0 / 39916800.0));
-    ps = fma(ps, z, kc(1.0 / 362880.0));
-    ps = fma(ps, z, kc(-1.0 / 5040.0));
-    ps = fma(ps, z, kc(1.0 / 120.0));
-    ps = fma(ps, z, kc(-1.0 / 6.0));
+    double ps = KC(1.0 / 355687428096000.0);
+    ps = fma(ps, z, KC(-1.0 / 1307674368000.0));
+    ps = fma(ps, z, KC(1.0 / 6227020800.0));
+    ps = fma(ps, z, KC(-1.0 / 39916800.0));
+    ps = fma(ps, z, KC(1.0 / 362880.0));
+    ps = fma(ps, z, KC(-1.0 / 5040.0));
+    ps = fma(ps, z, KC(1.0 / 120.0));
+    ps = fma(ps, z, KC(-1.0 / 6.0));
     s = fma(x * z, ps, x);
-    double pc = kc(-1.0 / 6402373705728000.0);
-    pc = fma(pc, z, kc(1.0 / 20922789888000.0));
-    pc = fma(pc, z, kc(-1.0 / 87178291200.0));
-    pc = fma(pc, z, kc(1.0 / 479001600.0));
-    pc = fma(pc, z, kc(-1.0 / 3628800.0));
-    pc = fma(pc, z, kc(1.0 / 40320.0));
-    pc = fma(pc, z, kc(-1.0 / 720.0));
-    pc = fma(pc, z, kc(1.0 / 24.0));
+    double pc = KC(-1.0 / 6402373705728000.0);
+    pc = fma(pc, z, KC(1.0 / 20922789888000.0));
+    pc = fma(pc, z, KC(-1.0 / 87178291200.0));
+    pc = fma(pc, z, KC(1.0 / 479001600.0));
+    pc = fma(pc, z, KC(-1.0 / 3628800.0));
+    pc = fma(pc, z, KC(1.0 / 40320.0));
+    pc = fma(pc, z, KC(-1.0 / 720.0));
+    pc = fma(pc, z, KC(1.0 / 24.0));
     pc = fma(pc, z, -0.5);
     c = fma(z, pc, 1.0);
 }
@@ -286,27 +309,47 @@ __host__ __device__ __forceinline__ void sincos_small(double x, double &s, doubl
 // W = [w]x of the unnormalised axis-angle w (|w| = theta), W^2 = w w^T - theta^2 I, so
 // helpers/utils.py:209-221's I + sin(theta) [w/theta]x + (1 - cos theta) [w/theta]x^2 is
 // cos(theta) I + (sin(theta)/theta) W + ((1 - cos theta)/theta^2) w w^T.
+#ifndef FMPNP_SO3_SHORT
+#define FMPNP_SO3_SHORT 1
+#endif
 __host__ __device__ __forceinline__ void so3_coeffs_small(double z, double &c, double &a, double &b) {
-    double pc = kc(1.0 / 6402373705728000.0);       // 1/18!
-    pc = fma(pc, -z, kc(1.0 / 20922789888000.0));  // 1/16!
-    pc = fma(pc, -z, kc(1.0 / 87178291200.0));
-    pc = fma(pc, -z, kc(1.0 / 479001600.0));
-    pc = fma(pc, -z, kc(1.0 / 3628800.0));
-    pc = fma(pc, -z, kc(1.0 / 40320.0));
-    pc = fma(pc, -z, kc(1.0 / 720.0));
-    pc = fma(pc, -z, kc(1.0 / 24.0));
+#if FMPNP_SO3_SHORT
+    if (z <= 2.5e-5) {
+        // theta <= 0.005 (an LM step near convergence): the series to z^4 -- the next terms are
+        // below z^5 / 11! = 2.5e-31 relative, far under the last bit -- with a third of the operations
+        double pb = fma(KC(1.0 / 3628800.0), -z, KC(1.0 / 40320.0));  // 1/10!, 1/8!
+        pb = fma(pb, -z, KC(1.0 / 720.0));
+        pb = fma(pb, -z, KC(1.0 / 24.0));
+        pb = fma(pb, -z, 0.5);
+        b = pb;
+        c = fma(pb, -z, 1.0);
+        double pa = fma(KC(1.0 / 362880.0), -z, KC(1.0 / 5040.0));  // 1/9!, 1/7!
+        pa = fma(pa, -z, KC(1.0 / 120.0));
+        pa = fma(pa, -z, KC(1.0 / 6.0));
+        a = fma(pa, -z, 1.0);
+        return;
+    }
+#endif
+    double pc = KC(1.0 / 6402373705728000.0);       // 1/18!
+    pc = fma(pc, -z, KC(1.0 / 20922789888000.0));  // 1/16!
+    pc = fma(pc, -z, KC(1.0 / 87178291200.0));
+    pc = fma(pc, -z, KC(1.0 / 479001600.0));
+    pc = fma(pc, -z, KC(1.0 / 3628800.0));
+    pc = fma(pc, -z, KC(1.0 / 40320.0));
+    pc = fma(pc, -z, KC(1.0 / 720.0));
+    pc = fma(pc, -z, KC(1.0 / 24.0));
     pc = fma(pc, -z, 0.5);                           // b = sum (-z)^k / (2k+2)!, k = 0..8
     b = pc;
     c = fma(pc, -z, 1.0);                            // cos = 1 - z b
-    double pa = kc(1.0 / 121645100408832000.0);     // 1/19!
-    pa = fma(pa, -z, kc(1.0 / 355687428096000.0));  // 1/17!
-    pa = fma(pa, -z, kc(1.0 / 1307674368000.0));
-    pa = fma(pa, -z, kc(1.0 / 6227020800.0));
-    pa = fma(pa, -z, kc(1.0 / 39916800.0));
-    pa = fma(pa, -z, kc(1.0 / 362880.0));
-    pa = fma(pa, -z, kc(1.0 / 5040.0));
-    pa = fma(pa, -z, kc(1.0 / 120.0));
-    pa = fma(pa, -z, kc(1.0 / 6.0));
+    double pa = KC(1.0 / 121645100408832000.0);     // 1/19!
+    pa = fma(pa, -z, KC(1.0 / 355687428096000.0));  // 1/17!
+    pa = fma(pa, -z, KC(1.0 / 1307674368000.0));
+    pa = fma(pa, -z, KC(1.0 / 6227020800.0));
+    pa = fma(pa, -z, KC(1.0 / 39916800.0));
+    pa = fma(pa, -z, KC(1.0 / 362880.0));
+    pa = fma(pa, -z, KC(1.0 / 5040.0));
+    pa = fma(pa, -z, KC(1.0 / 120.0));
+    pa = fma(pa, -z, KC(1.0 / 6.0));
     a = fma(pa, -z, 1.0);                            // sin(theta)/theta
 }
 
@@ -346,9 +389,9 @@ __host__ __device__ __forceinline__ void sincos_rr(double x, double &s, double &
         c = r.y;
         return;
     }
-    const double n = rint(x * kc(6.36619772367581382433e-01));  // 2 / pi
-    double r = fma(-n, kc(1.57079632673412561417e+00), x);      // pio2_1 (33 bits)
-    r = fma(-n, kc(6.07710050650619224932e-11), r);             // pio2_1t
+    const double n = rint(x * KC(6.36619772367581382433e-01));  // 2 / pi
+    double r = fma(-n, KC(1.57079632673412561417e+00), x);      // pio2_1 (33 bits)
+    r = fma(-n, KC(6.07710050650619224932e-11), r);             // pio2_1t
     double sr, cr;
     sincos_small(fabs(r), sr, cr);
     if (r < 0.0) sr = -sr;

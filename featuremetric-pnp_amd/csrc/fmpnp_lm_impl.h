@@ -56,6 +56,9 @@ constexpr bool kSpecBuild = FMPNP_SPEC != 0;
 #define FMPNP_STAMPS 0
 #endif
 constexpr bool kStamps = FMPNP_STAMPS != 0;
+#ifndef FMPNP_TAIL_T2
+#define FMPNP_TAIL_T2 0  // 1: branch-free combine + 16-byte pose stores (measured +1.4 % at B = 128, -0.6 % at B = 1)
+#endif
 
 // dynamic LDS of the LM kernel (the only kernel in this file that uses LDS)
 extern __shared__ __attribute__((aligned(16))) unsigned char lm_lds[];
@@ -171,6 +174,7 @@ struct LMState {
     Ctx c;
 };
 static_assert(sizeof(LMState) <= lds_fixed_bytes(), "LDS head too small");
+static_assert(offsetof(LMState, Ret) % 16 == 0, "Ret: 16-byte LDS writes of the next pose");
 
 __device__ __forceinline__ LMState &S() { return *reinterpret_cast<LMState *>(lm_lds); }
 
@@ -556,32 +560,35 @@ __device__ __forceinline__ void gather_half(const T *__restrict__ t, const T *__
     using VT = typename V16<T>::type;
     constexpr int V = V16<T>::n;
     if constexpr (VEC) {
-        if (ce - cb > 64 * V && ce - cb <= 128 * V) {
-            // 64 V < C <= 128 V (C = 512 fp32): all sixteen loads of the four rounds issued
-            // before the first use -- one memory round trip per point instead of two.  Rounds
-            // are consumed in the loop's (r, k) order, so the sums are the loop's bit for bit;
-            // missing rounds read round one again and add exact zeros.
-            const int c = cb + l32 * V;
-            VT f[4], x[4], y[4], q[4];
-            bool has[4];
+        if (ce - cb > 64 * V) {
+            // C > 64 V (C = 512 fp32, the pyramid's coarse level and cfg5; C = 1024 of the RobotCar
+            // hypercolumn's [640:1664] slice): chunks of four rounds whose sixteen loads are all
+            // issued before the first use -- one memory round trip per 128 V channels instead of
+            // one per 64 V.  Rounds are consumed in the loop's (r, k) order, so the sums are the
+            // loop's bit for bit; missing rounds read round one again and add exact zeros (a sum
+            // of fma(0, 0, s) steps from +0 is never -0: the zeros change no bit).
+            for (int c = cb + l32 * V; c < ce; c += 128 * V) {
+                VT f[4], x[4], y[4], q[4];
+                bool has[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                has[r] = c + r * 32 * V < ce;
-                const int cr = has[r] ? c + r * 32 * V : c;
-                f[r] = gload<VT>(t + cr);
-                x[r] = gload<VT>(t + cs + cr);
-                y[r] = gload<VT>(t + 2 * cs + cr);
-                q[r] = gload<VT>(rf + cr);
-            }
+                for (int r = 0; r < 4; ++r) {
+                    has[r] = c + r * 32 * V < ce;
+                    const int cr = has[r] ? c + r * 32 * V : c;
+                    f[r] = gload<VT>(t + cr);
+                    x[r] = gload<VT>(t + cs + cr);
+                    y[r] = gload<VT>(t + 2 * cs + cr);
+                    q[r] = gload<VT>(rf + cr);
+                }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const T *pf = reinterpret_cast<const T *>(&f[r]), *px = reinterpret_cast<const T *>(&x[r]);
-                const T *py = reinterpret_cast<const T *>(&y[r]), *pr = reinterpret_cast<const T *>(&q[r]);
+                for (int r = 0; r < 4; ++r) {
+                    const T *pf = reinterpret_cast<const T *>(&f[r]), *px = reinterpret_cast<const T *>(&x[r]);
+                    const T *py = reinterpret_cast<const T *>(&y[r]), *pr = reinterpret_cast<const T *>(&q[r]);
 #pragma unroll
-                for (int k = 0; k < V; ++k) {
-                    const double z = 0.0;
-                    acc6(a, has[r] ? (double)pf[k] : z, has[r] ? (double)pr[k] : z, has[r] ? (double)px[k] : z,
-                         has[r] ? (double)py[k] : z);
+                    for (int k = 0; k < V; ++k) {
+                        const double z = 0.0;
+                        acc6(a, has[r] ? (double)pf[k] : z, has[r] ? (double)pr[k] : z, has[r] ? (double)px[k] : z,
+                             has[r] ? (double)py[k] : z);
+                    }
                 }
             }
             return;
@@ -1845,6 +1852,18 @@ __device__ __forceinline__ double combine_final_wave(int mmax, bool team, bool s
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
     const int NC = c.NC;
     double t = 0.0;
+#if FMPNP_TAIL_T2
+    if (!team && NC <= 8) {
+        // (one round: four unconditional loads -- a missing chunk reads chunk 0 and adds nothing)
+        const double *src = lds_part(mmax, spec);
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = src[(h + 2 * u < NC ? h + 2 * u : 0) * NV + j];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (h + 2 * u < NC) t += v[u];
+    } else
+#endif
     if (!team) {
         const double *src = lds_part(mmax, spec);
         double v[4];
@@ -2167,11 +2186,23 @@ __device__ __forceinline__ void lm_step_store(const double *hs, double delta[6],
 #pragma unroll
     for (int k = 0; k < 3; ++k) tc[k] = base[9 + k];
     pose_update(Rc, tc, delta, Rn, tn);
+#if FMPNP_TAIL_T2
+    double2 *o = reinterpret_cast<double2 *>(st.Ret[nxt]);  // (16-byte aligned: six 16-byte LDS writes)
+    if (lane == 0) {
+        o[0] = make_double2(Rn[0], Rn[1]);
+        o[1] = make_double2(Rn[2], Rn[3]);
+        o[2] = make_double2(Rn[4], Rn[5]);
+        o[3] = make_double2(Rn[6], Rn[7]);
+        o[4] = make_double2(Rn[8], tn[0]);
+        o[5] = make_double2(tn[1], tn[2]);
+    }
+#else
     double *o = st.Ret[nxt];
     if (lane == 0) {
         for (int k = 0; k < 9; ++k) o[k] = Rn[k];
         for (int k = 0; k < 3; ++k) o[9 + k] = tn[k];
     }
+#endif
 }
 
 __device__ __forceinline__ double clip_lam(double l) { return l < 1e-6 ? 1e-6 : (l > 1e4 ? 1e4 : l); }
