@@ -59,7 +59,7 @@ LEGS = ["single", "hard", "ratio", "no_spec", "no_memo", "bilinear", "layout_f",
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8000)
+    ap.add_argument("--steps", type=int, default=30000)  # ~10 s timed: visible to a GPU-busy sampler
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=128, help="queries per GPU (weak scaling)")
     ap.add_argument("--global-batch", type=int, default=0,
