@@ -80,8 +80,12 @@ def rot_angle(Ra, Rb):
 # the blocking path packs f, gx, gy (fp32 gradients); the pipeline's default layout "f" forms
 # the gradients in fp64 in the LM gather -> the poses agree to the north-star tolerance
 dmax = max(rot_angle(a["R"], c["R"]) for x, z in zip(o1, o0) for a, c in zip(x, z))
+extra = {}
+for d in [int(x) for x in os.environ.get("DEPTHS", "").split(",") if x]:  # deeper slab rings
+    td, _ = run(d)
+    extra[f"pipelined_depth{d}_queries_per_s"] = round(NB * B / td, 1)
 print(json.dumps({"batches": NB, "batch": B, "queries": NB * B, "layout": "f", "blocking_s": round(t0, 4),
                   "blocking_queries_per_s": round(NB * B / t0, 1), "serial_s": round(t1, 4),
                   "pipelined_s": round(t2, 4), "serial_queries_per_s": round(NB * B / t1, 1),
                   "pipelined_queries_per_s": round(NB * B / t2, 1), "serial_equals_pipelined": same,
-                  "max_rot_diff_vs_blocking_fgrad_rad": dmax}))
+                  "max_rot_diff_vs_blocking_fgrad_rad": dmax, **extra}))
