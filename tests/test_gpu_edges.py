@@ -137,3 +137,29 @@ def test_bilinear_memo_one_team_walks_mixed_sizes():
         ores, _ = orc.forward(op, orc.make_options(12, 0.01, "geman_mcclure", sampling="bilinear"))
         np.testing.assert_allclose(r["R"], ores["R"], atol=1e-9)
         np.testing.assert_allclose(r["t"], ores["t"], atol=1e-9)
+
+
+@pytest.mark.parametrize("span", [256, 384, 512, 640, 1024])
+def test_vector_and_scalar_gathers_are_bit_identical(span):
+    """The gather's 16-byte vector form (aligned channel slice) and its scalar form (a slice
+    starting one channel into the 16-byte vector) accumulate every lane's channels in the same
+    (round, element) order, so the same channel values give the same six sums -- in every regime
+    of the vector form: one round pair (64 V = 256 fp32 channels), 64 V < C <= 128 V (384, 512),
+    and the chunks of four rounds above it (640: a ragged last chunk; 1024: the RobotCar
+    hypercolumn's [640:1664] slice).  Map B holds map A's channels shifted by three, so B's slice
+    [1, 1 + span) (scalar path) has A's slice [4, 4 + span) (vector path) channel for channel."""
+    N, H, W = 128, 24, 32
+    inp = synth.problem_inputs(N, span + 8, H, W, seed=61, device=DEV, init="hard")
+    fa, ra = inp["fmap"], inp["fref"]
+    fb = torch.cat([fa[3:], torch.zeros_like(fa[:3])])
+    rb = torch.cat([ra[:, 3:], torch.zeros_like(ra[:, :3])], 1)
+    args = (inp["pts3d"], inp["K"], inp["im_width"], inp["im_height"], inp["R0"], inp["t0"])
+    pa = rf.make_problem(rf.pack_features(fa, storage=torch.float32, device=DEV), ra, *args, 4, 4 + span)
+    pb = rf.make_problem(rf.pack_features(fb, storage=torch.float32, device=DEV), rb, *args, 1, 1 + span)
+    opts = rf.make_options(25, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32, wgs_per_problem=1)
+    (a,), (ta,) = rf.refine([pa], opts, trace=True)
+    (b,), (tb,) = rf.refine([pb], opts, trace=True)
+    assert ta["n_supported"].min() > 0
+    for k in ("cost", "n_supported", "accepted", "R", "t"):
+        assert np.array_equal(ta[k], tb[k]), k
+    assert np.array_equal(a["R"], b["R"]) and np.array_equal(a["t"], b["t"])
