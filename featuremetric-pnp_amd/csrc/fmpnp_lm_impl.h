@@ -56,6 +56,9 @@ constexpr bool kSpecBuild = FMPNP_SPEC != 0;
 #define FMPNP_STAMPS 0
 #endif
 constexpr bool kStamps = FMPNP_STAMPS != 0;
+#ifndef FMPNP_GEOM_EARLY
+#define FMPNP_GEOM_EARLY 0
+#endif
 #ifndef FMPNP_TAIL_T2
 #define FMPNP_TAIL_T2 0  // 1: branch-free combine + 16-byte pose stores (measured +1.4 % at B = 128, -0.6 % at B = 1)
 #endif
@@ -726,24 +729,37 @@ __device__ __forceinline__ constexpr int h_col(int k) {
 // One 64-point block of a wave: lane = point.  Points that do not contribute get w = 0
 // and a harmless geometry (z = 1).  Writes the block's partial (one chunk: LDS when
 // G == 1, the team's global slot `dst_g` with sc1 stores when G > 1).
-__device__ __forceinline__ void contrib_block(const PC &q, int mmax, int blk, bool sup, bool kept, double rho,
-                                              double d1, const double *r, int rs, const double Pc[3],
-                                              double *dst_g) {
-    const int lane = threadIdx.x & 63;
+// J_px_p (model.py:377-382) times J_p_T (model.py:369-370) of a point: A (2x6), A0[1] = A1[0] = 0
+// (a point that does not contribute gets the harmless geometry P = (0, 0, 1))
+struct Geo {
+    double A0[6], A1[6];
+};
+__device__ __forceinline__ Geo geo_of(const PC &q, bool kept, const double Pc[3]) {
     const double fx = q.fx, fy = q.fy;
-    const int lc = blk;  // one chunk per 64-point block
-    const double w = kept ? d1 : 0.0, rh = kept ? rho : 0.0;
     const double P0 = kept ? Pc[0] : 0.0, P1 = kept ? Pc[1] : 0.0, z = kept ? Pc[2] : 1.0;
-    // the point's record fields (SoA, stride rs): sum gx e, sum gy e, sum gx^2, sum gx gy, sum gy^2
-    const double sex = kept ? r[rs] : 0.0, sey = kept ? r[2 * rs] : 0.0;
-    const double sxx = kept ? r[3 * rs] : 0.0, sxy = kept ? r[4 * rs] : 0.0, syy = kept ? r[5 * rs] : 0.0;
-    // J_px_p (model.py:377-382) times J_p_T (model.py:369-370): A (2x6), A0[1] = A1[0] = 0
     // one reciprocal instead of six divisions (Jacobian entries only: last-bit level)
     const double iz = recip(z);
     const double j00 = fx * iz, j02 = ((-fx) * P0 * iz) * iz;
     const double j11 = fy * iz, j12 = ((-fy) * P1 * iz) * iz;
-    const double A0[6] = {j00, 0.0, j02, j02 * P1, j00 * z - j02 * P0, -j00 * P1};
-    const double A1[6] = {0.0, j11, j12, -j11 * z + j12 * P1, -j12 * P0, j11 * P0};
+    return Geo{{j00, 0.0, j02, j02 * P1, j00 * z - j02 * P0, -j00 * P1},
+               {0.0, j11, j12, -j11 * z + j12 * P1, -j12 * P0, j11 * P0}};
+}
+__device__ __forceinline__ void contrib_geo(const PC &q, int mmax, int blk, bool sup, bool kept, double rho,
+                                            double d1, const double *r, int rs, const Geo &G, double *dst_g);
+__device__ __forceinline__ void contrib_block(const PC &q, int mmax, int blk, bool sup, bool kept, double rho,
+                                              double d1, const double *r, int rs, const double Pc[3],
+                                              double *dst_g) {
+    contrib_geo(q, mmax, blk, sup, kept, rho, d1, r, rs, geo_of(q, kept, Pc), dst_g);
+}
+__device__ __forceinline__ void contrib_geo(const PC &q, int mmax, int blk, bool sup, bool kept, double rho,
+                                            double d1, const double *r, int rs, const Geo &G, double *dst_g) {
+    const int lane = threadIdx.x & 63;
+    const int lc = blk;  // one chunk per 64-point block
+    const double w = kept ? d1 : 0.0, rh = kept ? rho : 0.0;
+    // the point's record fields (SoA, stride rs): sum gx e, sum gy e, sum gx^2, sum gx gy, sum gy^2
+    const double sex = kept ? r[rs] : 0.0, sey = kept ? r[2 * rs] : 0.0;
+    const double sxx = kept ? r[3 * rs] : 0.0, sxy = kept ? r[4 * rs] : 0.0, syy = kept ? r[5 * rs] : 0.0;
+    const double *A0 = G.A0, *A1 = G.A1;
     // w folded into the 2x2 channel moments; the structural zeros A0[1] = A1[0] = 0 are
     // skipped explicitly (IEEE arithmetic cannot drop 0 * x by itself)
     const double wxx = w * sxx, wxy = w * sxy, wyy = w * syy, wex = w * sex, wey = w * sey;
@@ -1677,6 +1693,11 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         }
         dbg_stamp(q.stamps, 0);
         tl_stamp(q, 1);
+#if FMPNP_GEOM_EARLY
+        // the block's Jacobian geometry needs only the projection: formed before the gathers, so
+        // its instructions fill the wait for the changed texels instead of following it
+        const Geo geo = geo_of(q, off >= 0, Pc);
+#endif
         const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
         const bool wlane = (lane & 3) == 0 && e6 < 6;
         const size_t fo = (size_t)(wlane ? e6 : 0) * rs + blk * 64;  // this lane's field column
@@ -1703,7 +1724,11 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
             }
             if (sup) lmax = nanmax(lmax, fabs(rho));
         } else {
+#if FMPNP_GEOM_EARLY
+            contrib_geo(q, mmax, blk, sup, sup, rho, d1, r, rs, geo, dst_g);
+#else
             contrib_block(q, mmax, blk, sup, sup, rho, d1, r, rs, Pc, dst_g);
+#endif
         }
         dbg_stamp(q.stamps, 2);
         tl_stamp(q, 3);
@@ -2412,9 +2437,6 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
         if constexpr (kHelp) helper_run<T>(a, mmax);
         return;
     }
-#if defined(FMPNP_PRIO) && FMPNP_PRIO
-    if ((tid >> 6) >= 4) __builtin_amdgcn_s_setprio(1);  // experiment: the younger half first
-#endif
     for (int p = team; p < a.n; p += a.teams) {
         problem_begin(a.probs + p, p, mmax);
         PC q = load_pc();
