@@ -56,9 +56,6 @@ constexpr bool kSpecBuild = FMPNP_SPEC != 0;
 #define FMPNP_STAMPS 0
 #endif
 constexpr bool kStamps = FMPNP_STAMPS != 0;
-#ifndef FMPNP_GEOM_EARLY
-#define FMPNP_GEOM_EARLY 0
-#endif
 #ifndef FMPNP_TAIL_T2
 #define FMPNP_TAIL_T2 0  // 1: branch-free combine + 16-byte pose stores (measured +1.4 % at B = 128, -0.6 % at B = 1)
 #endif
@@ -1693,11 +1690,6 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         }
         dbg_stamp(q.stamps, 0);
         tl_stamp(q, 1);
-#if FMPNP_GEOM_EARLY
-        // the block's Jacobian geometry needs only the projection: formed before the gathers, so
-        // its instructions fill the wait for the changed texels instead of following it
-        const Geo geo = geo_of(q, off >= 0, Pc);
-#endif
         const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
         const bool wlane = (lane & 3) == 0 && e6 < 6;
         const size_t fo = (size_t)(wlane ? e6 : 0) * rs + blk * 64;  // this lane's field column
@@ -1724,11 +1716,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
             }
             if (sup) lmax = nanmax(lmax, fabs(rho));
         } else {
-#if FMPNP_GEOM_EARLY
-            contrib_geo(q, mmax, blk, sup, sup, rho, d1, r, rs, geo, dst_g);
-#else
             contrib_block(q, mmax, blk, sup, sup, rho, d1, r, rs, Pc, dst_g);
-#endif
         }
         dbg_stamp(q.stamps, 2);
         tl_stamp(q, 3);
@@ -2439,34 +2427,39 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
     }
     for (int p = team; p < a.n; p += a.teams) {
         problem_begin(a.probs + p, p, mmax);
-        PC q = load_pc();
-        q.helpers = kHelp ? a.helpers : 0;
-        q.prob = p;
-        q.hrec = a.hrec;
-        q.hflag = a.hflag;
-        q.htag = a.htag;
-        q.tl = (kStamps && a.stamps != nullptr && (a.dbg & 16) && p == team) ? a.stamps + (size_t)blockIdx.x * 8 * 16
-                                                                             : nullptr;
-        q.tl_eval = a.dbg >> 8;
-        q.cur_eval = -1;
-        bool first_eval = true;
-        if constexpr (!TEAM) {  // one workgroup: it owns every chunk (compile-time constants)
-            q.G = 1;
-            q.c0 = 0;
-            q.p0 = 0;
-        }
-        q.use_ratio = RATIO ? 1 : 0;
         // speculation: the nearest-sampling variants of the latency build.  The planner runs a
         // _SPEC variant exactly when it enables speculation (memoised), so the flag is a constant
         constexpr bool kSpec = kSpecBuild && WPS == WPS_LATENCY &&
                                (VAR == VAR_GM_SPEC || VAR == VAR_NEAREST_SPEC || VAR == VAR_GM_SPEC_H ||
                                 VAR == VAR_NEAREST_SPEC_H);
-        q.spec = kSpec ? 1 : 0;
-        if constexpr (kSpec) q.no_memo = 0;
-        if constexpr (VAR == VAR_GM || VAR == VAR_F_GM || VAR == VAR_GM_SPEC || VAR == VAR_GM_SPEC_H ||
-                      VAR == VAR_GM_H)
-            q.loss = FMPNP_GEMAN_MCCLURE;
-        q.bilinear = (VAR == VAR_BILINEAR || VAR == VAR_BIL_DIRECT) ? 1 : 0;
+        // the problem's constants in registers (from the LDS Ctx), with this variant's constants
+        auto make_q = [&]() {
+            PC r = load_pc();
+            r.helpers = kHelp ? a.helpers : 0;
+            r.prob = p;
+            r.hrec = a.hrec;
+            r.hflag = a.hflag;
+            r.htag = a.htag;
+            r.tl = (kStamps && a.stamps != nullptr && (a.dbg & 16) && p == team) ? a.stamps + (size_t)blockIdx.x * 8 * 16
+                                                                                 : nullptr;
+            r.tl_eval = a.dbg >> 8;
+            r.cur_eval = -1;
+            if constexpr (!TEAM) {  // one workgroup: it owns every chunk (compile-time constants)
+                r.G = 1;
+                r.c0 = 0;
+                r.p0 = 0;
+            }
+            r.use_ratio = RATIO ? 1 : 0;
+            r.spec = kSpec ? 1 : 0;
+            if constexpr (kSpec) r.no_memo = 0;
+            if constexpr (VAR == VAR_GM || VAR == VAR_F_GM || VAR == VAR_GM_SPEC || VAR == VAR_GM_SPEC_H ||
+                          VAR == VAR_GM_H)
+                r.loss = FMPNP_GEMAN_MCCLURE;
+            r.bilinear = (VAR == VAR_BILINEAR || VAR == VAR_BIL_DIRECT) ? 1 : 0;
+            return r;
+        };
+        PC q = make_q();
+        bool first_eval = true;
         long long ngath = 0;  // texel gathers of this wave for this problem
         int k = 0;  // evaluations completed: the next one reads sc[k & 1] and Ret[k & 1]
         while (true) {
