@@ -313,26 +313,29 @@ __device__ __forceinline__ void pose_update(const double *R, const double *t, co
                                             double *tn) {
     const double w0 = delta[3], w1 = delta[4], w2 = delta[5];
     const double z = fma(w2, w2, fma(w1, w1, w0 * w0));
-    double dR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-    if (isnan(z)) {
+    double dR[9];
+    // (the common case first and alone: no identity / NaN matrix materialised on its path)
+    if (z >= 1e-24 && z <= 0.61685027506808487) {  // 1e-12 <= theta <= pi/4 (false for NaN)
+        double cz, az, bz;
+        so3_coeffs_small(z, cz, az, bz);
+        const double bw0 = bz * w0, bw1 = bz * w1, bw2 = bz * w2;
+        const double aw0 = az * w0, aw1 = az * w1, aw2 = az * w2;
+        dR[0] = fma(bw0, w0, cz);
+        dR[1] = fma(bw0, w1, -aw2);
+        dR[2] = fma(bw0, w2, aw1);
+        dR[3] = fma(bw1, w0, aw2);
+        dR[4] = fma(bw1, w1, cz);
+        dR[5] = fma(bw1, w2, -aw0);
+        dR[6] = fma(bw2, w0, -aw1);
+        dR[7] = fma(bw2, w1, aw0);
+        dR[8] = fma(bw2, w2, cz);
+    } else if (isnan(z)) {
 #pragma unroll
         for (int i = 0; i < 9; ++i) dR[i] = NAN;
-    } else if (!(z < 1e-24)) {  // theta >= 1e-12 (below: the identity, as the reference)
-        if (z <= 0.61685027506808487) {  // (pi/4)^2
-            double cz, az, bz;
-            so3_coeffs_small(z, cz, az, bz);
-            const double bw0 = bz * w0, bw1 = bz * w1, bw2 = bz * w2;
-            const double aw0 = az * w0, aw1 = az * w1, aw2 = az * w2;
-            dR[0] = fma(bw0, w0, cz);
-            dR[1] = fma(bw0, w1, -aw2);
-            dR[2] = fma(bw0, w2, aw1);
-            dR[3] = fma(bw1, w0, aw2);
-            dR[4] = fma(bw1, w1, cz);
-            dR[5] = fma(bw1, w2, -aw0);
-            dR[6] = fma(bw2, w0, -aw1);
-            dR[7] = fma(bw2, w1, aw0);
-            dR[8] = fma(bw2, w2, cz);
-        } else {
+    } else {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) dR[i] = (i % 4 == 0) ? 1.0 : 0.0;
+        if (!(z < 1e-24)) {  // theta > pi/4 (below 1e-12: the identity, as the reference)
             const double theta = sqrt(z);
             const double it = 1.0 / theta;
             const double k0 = w0 * it, k1 = w1 * it, k2 = w2 * it;
