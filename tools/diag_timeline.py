@@ -21,7 +21,8 @@ for q in range(B):
     feats = rf.pack_features(inp["fmap"], storage=torch.float32, device=dev)
     probs.append(rf.make_problem(feats, inp["fref"], inp["pts3d"], inp["K"], inp["im_width"], inp["im_height"],
                                  inp["R0"], inp["t0"]))
-opts = rf.make_options(50, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32)
+ratio = float(os.environ["RATIO"]) if os.environ.get("RATIO") else None  # ratio test (model.py:324-336)
+opts = rf.make_options(50, 0.01, _lib.GEMAN_MCCLURE, ratio_threshold=ratio, dtype=_lib.F32)
 ab = rf.AsyncBatch(probs, opts)
 for _ in range(3):
     ab.launch()
