@@ -421,7 +421,7 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
         // (read per launch: measurement and test knobs, FMPNP_SPEC_CAP / FMPNP_SPEC_W0)
         const char *ec = getenv("FMPNP_SPEC_CAP"), *ew = getenv("FMPNP_SPEC_W0");
         a.spec_cap = ec ? std::max(0, atoi(ec)) : 2;
-        a.spec_w0 = ew ? std::max(0, atoi(ew)) : 4;
+        a.spec_w0 = ew ? std::max(0, atoi(ew)) : 3;  // round 3: wave 3 (no tail role) speculates too
     }
     {
         const char *e = getenv("FMPNP_DBG");  // debug knob, read per launch (fmpnp_internal.h LaunchArgs::dbg)

@@ -5,13 +5,13 @@
 
 #include "fmpnp.h"
 
-// Speculative next-texel gathers (fmpnp_lm_impl.h spec_pass; variants VAR_*_SPEC), on the later wave of each SIMD
-// only (waves >= spec_w0 = 4) and at most spec_cap = 2 per wave per evaluation: those waves
-// finish their point phase after their SIMD partners, so their changed texels are the ones
-// worth taking off the evaluation, and two gathers fit in wave 0's LM tail (round 3, B=128:
-// cap 2 0.332 ms, cap 1 / 3 / 4 0.341 / 0.344 / 0.340; every wave speculating, the tail waves'
-// blocks adopted by waves 3, 5, 6: 0.385 -- DESIGN.md §4.1.1).  Build with -DFMPNP_SPEC=0 to
-// compile them out.
+// Speculative next-texel gathers (fmpnp_lm_impl.h spec_pass; variants VAR_*_SPEC), on the waves
+// without an LM-tail role (waves >= spec_w0 = 3: the later wave of each SIMD, which finishes its
+// point phase after its SIMD partner, and wave 3, idle in the tail) and at most spec_cap = 2 per
+// wave per evaluation, which fit in wave 0's LM tail (round 3, B=128: spec_w0 3 / 4 / 5 / 6
+// 0.331 / 0.333 / 0.337 / 0.342 ms; cap 2 0.332 ms, cap 1 / 3 / 4 0.341 / 0.344 / 0.340; every
+// wave speculating, the tail waves' blocks adopted by waves 3, 5, 6: 0.385 -- DESIGN.md §4.1.1).
+// Build with -DFMPNP_SPEC=0 to compile them out.
 #ifndef FMPNP_SPEC
 #define FMPNP_SPEC 1
 #endif
