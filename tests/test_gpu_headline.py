@@ -152,10 +152,10 @@ def test_speculative_gathers_change_nothing(layout, init, ratio, wgs):
     assert c["texel_gathers"] >= b["texel_gathers"]
 
 
-@pytest.mark.parametrize("w0,cap", [("0", "4"), ("1", "64"), ("4", "0"), ("4", "2"), ("4", "4"), ("8", "4")])
+@pytest.mark.parametrize("w0,cap", [("0", "4"), ("1", "64"), ("3", "2"), ("4", "0"), ("4", "2"), ("4", "4"), ("8", "4")])
 def test_speculation_settings_change_nothing(w0, cap, monkeypatch):
-    """Which waves speculate (FMPNP_SPEC_W0: the default 4 is the later wave of each SIMD; 0
-    adds wave 0's held pair; 8 none) and how many texels each gathers per evaluation
+    """Which waves speculate (FMPNP_SPEC_W0: the default 3 adds wave 3, idle in the tail, to the
+    later wave of each SIMD; 0 adds wave 0's held pair; 8 none) and how many texels each gathers per evaluation
     (FMPNP_SPEC_CAP; a withdrawn prediction is gathered on demand) only move where sums come
     from: bit-identical to the run without speculation."""
     if not _lib.spec_build():
