@@ -2519,8 +2519,9 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
                 tl_stamp(q, 9);
             }
             // speculative gathers of the predicted next texels (spec_pass), while wave 0 finishes the
-            // tail: each wave >= 1 for its own blocks (waves 1 and 2 after their tail roles), and wave
-            // 3 -- idle in the tail -- for wave 0's blocks too.  Their channel sums then leave the next
+            // tail: each wave >= max(1, spec_w0) for its own blocks (default spec_w0 = 3: wave 3, idle
+            // in the tail, and waves 4-7; waves 1 and 2 after their tail roles when spec_w0 <= 2), and
+            // with spec_w0 = 0 wave 3 for wave 0's blocks too.  Their channel sums then leave the next
             // evaluation's point phase, which issue-bounds the SIMDs.
             if (kSpec && q.spec) {
                 if (wave >= 1 && wave >= q.spec_w0) {
