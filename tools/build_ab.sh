@@ -19,10 +19,13 @@ if [ -n "$rev" ]; then
   src=$tmp/featuremetric-pnp_amd/csrc
   inc=$tmp/include
 fi
+rm -f "$out"/*.o "$out/libfmpnp.so"
+pids=""
 for f in fmpnp_lm fmpnp_lm_f32 fmpnp_lm_f64 fmpnp_pack fmpnp_points fmpnp_api; do
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -I"$inc" -I"$src" "$@" -c -o "$out/$f.o" "$src/$f.hip" &
+  pids="$pids $!"
 done
-wait
+for p in $pids; do wait "$p" || { echo "compile failed"; exit 1; }; done
 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -shared -o "$out/libfmpnp.so" "$out"/*.o
 rm -f "$out"/*.o
 echo "built $out/libfmpnp.so ${rev:+from $rev}"
