@@ -121,19 +121,35 @@ def workload_tag(B, init, ratio, memo, sampling, layout, spec=True):
     return t
 
 
-def load_traffic(tag):
-    """(HBM bytes per launch, kernel name, rocprof avg ns) of a workload from its committed
-    rocprofv3 PMC summary, or (None, None, None)."""
-    for rnd in ("r03", "r02"):  # the newest round's profile of the workload
+PROFILE_ROUNDS = ("r04", "r03", "r02")  # newest first
+
+
+def load_traffic(tag, kernel, digest, root=ROOT):
+    """HBM bytes per launch of this workload from a committed rocprofv3 FETCH_SIZE / WRITE_SIZE
+    summary (profiles/rNN_pmc_<tag>.json), accepted only when it was taken of the kernel
+    specialisation this launch ran (`kernel`, e.g. fmpnp::lm_kernel<float, 2, false, false, 6>)
+    AND with the sources the loaded library was built from (`digest`, fmpnp_build_info).
+    Returns (bytes, kernel, rocprof avg ns, path, why-not): a profile of another variant, of an
+    older build, or without a recorded digest is never used -- the roofline then counts the
+    kernel's own gathered bytes and says why."""
+    rejected = []
+    for rnd in PROFILE_ROUNDS:
         path = os.path.join("profiles", f"{rnd}_pmc_{tag}.json")
         try:
-            with open(os.path.join(ROOT, path)) as f:
+            with open(os.path.join(root, path)) as f:
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        name = (d.get("kernel") or "").replace("void ", "").replace("(fmpnp::LaunchArgs)", "")
-        return d.get("hbm_bytes_per_launch"), name or None, d.get("kernel_avg_ns"), path
-    return None, None, None, None
+        name = (d.get("kernel") or "").replace("void ", "").replace("(fmpnp::LaunchArgs)", "").strip()
+        if name != kernel:
+            rejected.append(f"{path}: kernel {name or '?'} is not the launch's {kernel}")
+        elif digest == "unknown" or d.get("source_digest") != digest:
+            rejected.append(f"{path}: taken with sources {d.get('source_digest')}, the loaded library is {digest}")
+        elif not d.get("hbm_bytes_per_launch"):
+            rejected.append(f"{path}: no FETCH/WRITE bytes")
+        else:
+            return d["hbm_bytes_per_launch"], name, d.get("kernel_avg_ns"), path, None
+    return None, None, None, None, ("; ".join(rejected) or f"no profiles/rNN_pmc_{tag}.json")
 
 
 def gather_bytes_rule(sampling, layout):
@@ -145,19 +161,24 @@ def gather_bytes_rule(sampling, layout):
     return 16 * C, "(f, gx, gy, fref) x 4C per gather"
 
 
-def roofline(tag, res, kernel_s, B, sampling, layout):
+def roofline(tag, res, kernel_s, B, sampling, layout, launch):
+    from fmpnp import _lib
     per_gather, rule = gather_bytes_rule(sampling, layout)
     gathers = int(sum(r["texel_gathers"] for r in res))
     n_evals = int(sum(r["n_evals"] for r in res))
     gathered = gathers * per_gather + B * N_PTS * 24
-    traffic, kname, prof_ns, prof_path = load_traffic(tag)
+    kernel = _lib.kernel_name(launch)
+    digest = _lib.library_digest()
+    traffic, kname, prof_ns, prof_path, why_not = load_traffic(tag, kernel, digest)
     ach_bytes = traffic if traffic else gathered
     ach = ach_bytes / kernel_s
     return {"bound": "hbm", "achieved": round(ach / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK, 4), "traffic": traffic,
-            "achieved_source": ("rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, %s" % prof_path) if traffic
-            else "texel gathers counted by the kernel x bytes per gather (no matching PMC profile)",
-            "kernel": kname or "fmpnp::lm_kernel", "avg_kernel_ms": round(kernel_s * 1e3, 4),
+            "achieved_source": ("rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, %s (kernel and source digest %s match "
+                                "this launch)" % (prof_path, digest)) if traffic
+            else "LIVE gathered bytes (texel gathers counted by the kernel x bytes per gather): no committed PMC "
+                 "profile of this kernel and build (%s)" % why_not,
+            "kernel": kernel, "source_digest": digest, "avg_kernel_ms": round(kernel_s * 1e3, 4),
             "rocprof_avg_kernel_ms": round(prof_ns / 1e6, 4) if prof_ns else None,
             "gathered_bytes_per_launch": gathered, "gathered_GB_per_s": round(gathered / kernel_s / 1e9, 1),
             "gathered_bytes_rule": rule + " + 24 B fp64 point per query point",
@@ -175,20 +196,29 @@ def main():
     if world != args.gpus:
         log(f"[bench] error: --gpus {args.gpus} but the launcher started {world} ranks (WORLD_SIZE)")
         sys.exit(2)
-    if os.environ.get("FMPNP_BENCH_DRYRUN"):  # CPU test of the launch path: report the rank, touch no GPU
-        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": world,
-                          "queries": list(__import__("fmpnp.shard", fromlist=["x"]).query_indices(
-                              int(os.environ.get("RANK", "0")), world, per_rank=args.batch,
-                              global_batch=args.global_batch))}), flush=True)
-        return
+    dryrun = bool(os.environ.get("FMPNP_BENCH_DRYRUN"))  # CPU test of the launch path: touch no GPU
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
     # one process per GPU; FMPNP_BENCH_BACKEND=gloo (and more ranks than GPUs) rehearses the
-    # distributed path on a one-GPU box -- the timing barrier and max-over-ranks only
+    # distributed path on a one-GPU box -- the timing barrier and max-over-ranks only, reported as
+    # a rehearsal with n_gpus = the distinct devices used (never a multi-GPU figure)
     backend = os.environ.get("FMPNP_BENCH_BACKEND", "nccl")
-    ndev = max(1, torch.cuda.device_count())
+    # (device_count() does not initialise the GPU on this image; FMPNP_BENCH_NDEV: dry runs only)
+    ndev = (int(os.environ.get("FMPNP_BENCH_NDEV", "1")) if dryrun else 0) or max(1, torch.cuda.device_count())
+    if dist and backend == "nccl" and world > ndev:
+        log(f"[bench] error: {world} ranks but {ndev} visible GPU(s): one process per GPU (rehearse more ranks "
+            f"with FMPNP_BENCH_BACKEND=gloo)")
+        sys.exit(3)
     gpu = local % ndev
+    if dryrun:
+        from fmpnp import shard as _sh
+        n_gpus, rpd = _sh.device_accounting([r % ndev for r in range(world)])  # single node: LOCAL_RANK = RANK
+        print(json.dumps({"rank": rank, "world": world, "device": gpu, "n_gpus": n_gpus, "ranks": world,
+                          "ranks_per_device": rpd,
+                          "queries": list(_sh.query_indices(rank, world, per_rank=args.batch,
+                                                            global_batch=args.global_batch))}), flush=True)
+        return
     if dist:
         import torch.distributed as tdist
         if backend == "nccl":
@@ -247,6 +277,10 @@ def main():
         e1.record(stream)
 
     elapsed = shard.timed_steps(step, args.steps, device=dev)
+    props = torch.cuda.get_device_properties(dev)
+    my_dev = (__import__("socket").gethostname(), getattr(props, "pci_domain_id", 0), getattr(props, "pci_bus_id", gpu),
+              getattr(props, "pci_device_id", 0))
+    n_gpus, ranks_per_device = shard.device_accounting(shard.gather_device_ids(my_dev))
     kernel_s = float(np.mean([a.elapsed_time(b) for a, b in ev])) / 1e3
     res = batch.results()
     statuses = sorted({r["status"] for r in res})
@@ -266,7 +300,7 @@ def main():
             "metric": "pose-refinements/sec (N=512 pts, C=256, 240x320, 50 LM iters)",
             "value": round(value, 3),
             "unit": "pose-refinements/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,  # distinct devices used (ranks sharing a GPU count once)
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 4),
@@ -286,14 +320,17 @@ def main():
                        "sampling": args.sampling, "layout": args.layout,
                        "batch_per_gpu": B, "global_batch": total,
                        "parallelism": f"query sharding x{world} (no collectives)", "launch": launch,
-                       "ranks": world, "devices_visible": ndev,
+                       "ranks": world, "ranks_per_device": ranks_per_device, "devices_visible": ndev,
                        "backend": (backend if dist else None)},
             "gn_iters_per_s": round(value * ITERS, 1),
-            "roofline": roofline(tag, res, kernel_s, B, args.sampling, args.layout),
+            "roofline": roofline(tag, res, kernel_s, B, args.sampling, args.layout, launch),
             "kernel_timing": f"HIP events on the launch stream around every {every}-th of the {args.steps} timed "
                              f"launches ({len(ev)} samples)",
             "statuses": statuses,
         }
+        if ranks_per_device > 1:
+            out["rehearsal"] = (f"{world} ranks on {n_gpus} device(s): a rehearsal of the distributed path "
+                                f"(barrier + max-over-ranks timing), not a multi-GPU scaling figure")
         out.update(extras)
         print(json.dumps(out), flush=True)
     if dist:
@@ -321,10 +358,12 @@ def rot_angle(Ra, Rb):
 
 
 def leg_summary(tag, ms, res, B, sampling="nearest", layout="fgrad", base=None):
+    """(call right after the leg's launches: its roofline matches profiles against last_launch())"""
+    from fmpnp import _lib
     rf_s = B / (ms / 1e3)
     d = {"ms_per_launch": round(ms, 4), "pose_refinements_per_s": round(rf_s, 1),
          "gn_iters_per_s": round(rf_s * ITERS, 1), "statuses": sorted({r["status"] for r in res}),
-         "roofline": roofline(tag, res, ms / 1e3, B, sampling, layout)}
+         "roofline": roofline(tag, res, ms / 1e3, B, sampling, layout, _lib.last_launch())}
     if base is not None:
         d["max_rot_diff_vs_headline_rad"] = float(max(rot_angle(a["R"], b["R"]) for a, b in zip(res, base)))
         d["poses_bit_identical_to_headline"] = bool(all(np.array_equal(a["R"], b["R"]) and

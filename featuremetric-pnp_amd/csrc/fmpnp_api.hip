@@ -239,9 +239,13 @@ int fmpnp_abi_version(void) { return FMPNP_ABI_VERSION; }
 
 #define FMPNP_STR2(x) #x
 #define FMPNP_STR(x) FMPNP_STR2(x)
+#ifndef FMPNP_SOURCE_DIGEST
+#define FMPNP_SOURCE_DIGEST "unknown"  // (builds outside the Makefile, e.g. tools/build_ab.sh)
+#endif
 const char *fmpnp_build_info(void) {
     return "fmpnp gfx950: lm_kernel(NT=512 wave-owned blocks, CH=64, NV=32, fp64 accumulation, bilinear cell memo), "
-           "pack_kernel(Sobel+HWC3), gather_ref_kernel; speculative_gathers=" FMPNP_STR(FMPNP_SPEC);
+           "pack_kernel(Sobel+HWC3), gather_ref_kernel; speculative_gathers=" FMPNP_STR(FMPNP_SPEC)
+           "; source_digest=" FMPNP_SOURCE_DIGEST;
 }
 
 int fmpnp_device_check(int device) {

@@ -79,7 +79,10 @@ __device__ __forceinline__ double wave_nanmax(double v) {
 
 // 1/x by v_rcp_f64 and two Newton steps (about 0.5 ulp; not always the correctly rounded
 // quotient): used where the reference's division only feeds weights, Jacobians or the
-// mean cost, never a pixel rounding.
+// mean cost -- and by project_pc (fmpnp_lm_impl.h) for the nearest path's rounded pixel, behind
+// a guard: a quotient within 2^-49 relative of a half-integer (rint's boundary), a z outside
+// [2^-1000, 2^1000] or a non-finite quotient takes the exact IEEE division instead.  A change to
+// this function's precision must re-check that guard's bound.
 __device__ __forceinline__ double recip(double x) {
     double r = __builtin_amdgcn_rcp(x);
     r = fma(fma(-x, r, 1.0), r, r);

@@ -65,7 +65,14 @@ struct LaunchArgs {
 constexpr int HREC = 7;
 
 // Fixed LDS head: the LM state + per-problem context (sized generously, 16-B aligned).
-__host__ __device__ constexpr int lds_fixed_bytes() { return 4096; }
+// Debug instrumentation (phase stamps, per-evaluation stamps, the evaluation timeline) exists only
+// in a diagnostics build (-DFMPNP_STAMPS=1 on every unit, tools/build_ab.sh); its LDS arrays then
+// enlarge the head below, so every unit must see the same value.
+#ifndef FMPNP_STAMPS
+#define FMPNP_STAMPS 0
+#endif
+// LDS head of the LM kernel (LMState, fmpnp_lm_impl.h): 2 KB in the product build
+__host__ __device__ constexpr int lds_fixed_bytes() { return FMPNP_STAMPS ? 4096 : 2304; }
 // row stride (doubles) of the LM kernel's structure-of-arrays LDS records: odd, so the
 // writers of one point's fields fall in distinct banks (fmpnp_lm_impl.h lds_X / lds_rec)
 __host__ __device__ constexpr int lds_rs(int mmax) { return mmax + 1; }

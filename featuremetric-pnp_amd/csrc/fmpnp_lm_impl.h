@@ -52,9 +52,7 @@ constexpr bool kSpecBuild = FMPNP_SPEC != 0;
 // Debug instrumentation (fmpnp_debug_stamps: phase totals, per-evaluation stamps, the evaluation
 // timeline) is compiled in only with -DFMPNP_STAMPS=1 (a diagnostics build, tools/build_ab.sh):
 // its flags and pointers would otherwise hold scalar registers across the evaluation loop.
-#ifndef FMPNP_STAMPS
-#define FMPNP_STAMPS 0
-#endif
+// (FMPNP_STAMPS itself is defined in fmpnp_internal.h: it also sizes the LDS head)
 constexpr bool kStamps = FMPNP_STAMPS != 0;
 #ifndef FMPNP_TAIL_T2
 #define FMPNP_TAIL_T2 0  // 1: branch-free combine + 16-byte pose stores (measured +1.4 % at B = 128, -0.6 % at B = 1)
@@ -166,11 +164,16 @@ struct LMState {
     LMScal sc[2];
     double rho_max;
     int abort_flag, sync_ok;
+    int helper_absent;      // a first-evaluation helper never published: the other blocks skip the wait
+#if FMPNP_STAMPS
     unsigned long long tlb[NT / 64][16];  // debug timeline (FMPNP_DBG bit 4), flushed at problem end
+#endif
     double wg_max[NT / 64];
     unsigned long long bil_dirty[BIL_MAX_M / 64];  // bilinear memo: each block's points whose cell changed
     long long wg_gath[NT / 64];                     // per-wave texel gathers of the problem (G = 1)
+#if FMPNP_STAMPS
     unsigned long long stamp_t[NT / 64], stamp_ph[NT / 64][NSTAMP];  // debug phase stamps (lane 0 per wave)
+#endif
     Ctx c;
 };
 static_assert(sizeof(LMState) <= lds_fixed_bytes(), "LDS head too small");
@@ -216,17 +219,21 @@ __device__ __forceinline__ PC load_pc() {
 // debug: add the cycles since the wave's previous stamp to its phase k (lane 0 of each
 // wave); phases 0..3 of the first evaluation go to slots 8..11
 __device__ __forceinline__ void dbg_stamp(bool on, int k) {
+#if FMPNP_STAMPS
     LMState &st = *reinterpret_cast<LMState *>(lm_lds);
-    if (kStamps && on && (threadIdx.x & 63) == 0) {
+    if (on && (threadIdx.x & 63) == 0) {
         const int w = threadIdx.x >> 6;
         const unsigned long long now = __builtin_amdgcn_s_memtime();
         st.stamp_ph[w][k < 4 && st.sc[1].n_evals == 0 ? 8 + k : k] += now - st.stamp_t[w];
         st.stamp_t[w] = now;
     }
+#endif
 }
 __device__ __forceinline__ void tl_stamp(const PC &q, int k) {
-    if (kStamps && q.tl && q.cur_eval == q.tl_eval && (threadIdx.x & 63) == 0)
+#if FMPNP_STAMPS
+    if (q.tl && q.cur_eval == q.tl_eval && (threadIdx.x & 63) == 0)
         reinterpret_cast<LMState *>(lm_lds)->tlb[threadIdx.x >> 6][k] = __builtin_amdgcn_s_memtime();
+#endif
 }
 // project_px (fmpnp_device.h) for the problem's K.  With a pinhole K the products of its zero
 // entries are dropped: (fx P0 + 0 P1) + cx P2 equals fx P0 + cx P2 and (0 P0 + 0 P1) + 1 P2
@@ -468,6 +475,7 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
             sc.nan = 0;
         }
         st.abort_flag = 0;
+        st.helper_absent = 0;
     }
     __syncthreads();
     // this workgroup's points -> LDS once per problem
@@ -479,7 +487,9 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
     for (int e = tid; e < 3 * c.M; e += nt) X[(e % 3) * rs + e / 3] = src[e];
     int *tex = lds_tex(mmax, c.spec);
     for (int i = tid; i < mmax; i += nt) tex[i] = -2;  // no texel cached yet
+#if FMPNP_STAMPS
     for (int i = tid; i < (NT / 64) * 16; i += nt) st.tlb[i >> 4][i & 15] = 0;  // debug timeline
+#endif
     if (c.spec) {
         int *tex2 = lds_tex2(mmax, true), *slot = lds_slot(mmax, true), *spec = lds_spec(mmax, true);
         float *qp = lds_qp(mmax, true);
@@ -496,8 +506,10 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
 // k: the evaluations completed (the state is sc[k & 1])
 __device__ __forceinline__ void problem_end(bool own_gathers, int k, unsigned long long *tl) {
     LMState &st = S();
+#if FMPNP_STAMPS
     if (tl && (threadIdx.x & 63) == 0)  // debug timeline: this wave's stamps
         for (int j = 0; j < 16; ++j) tl[(threadIdx.x >> 6) * 16 + j] = st.tlb[threadIdx.x >> 6][j];
+#endif
     if (threadIdx.x == 0) {
         LMScal &sc = st.sc[k & 1];
         if (st.abort_flag) {
@@ -1666,11 +1678,17 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
             const unsigned long long *flag = q.hflag + (size_t)q.prob * q.nc_max + blk;
             int ok = 1;
             if (lane == 0) {
+                // one bounded wait per workgroup: once any block's helper has timed out, the other
+                // blocks gather themselves at once (so the whole problem waits at most 0.2 s)
+                if (*reinterpret_cast<volatile int *>(&st.helper_absent)) ok = 0;
                 const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                while (__hip_atomic_load(reinterpret_cast<const g_u64 *>(reinterpret_cast<uintptr_t>(flag)),
-                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != q.htag) {
+                while (ok && __hip_atomic_load(reinterpret_cast<const g_u64 *>(reinterpret_cast<uintptr_t>(flag)),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != q.htag) {
                     __builtin_amdgcn_s_sleep(1);
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) { ok = 0; break; }  // 0.2 s
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 0.2 s
+                        ok = 0;
+                        *reinterpret_cast<volatile int *>(&st.helper_absent) = 1;
+                    }
                 }
                 // a helper that never published (kept from being resident by other kernels): the
                 // block is gathered here as usual; reported, results unaffected
@@ -2413,15 +2431,17 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
     }
     __syncthreads();
     // optional phase stamps (debug: a.stamps != null): s_memtime deltas on thread 0
-    const bool stamps_on = kStamps && a.stamps != nullptr && !(a.dbg & 20);
+    [[maybe_unused]] const bool stamps_on = kStamps && a.stamps != nullptr && !(a.dbg & 20);
     // debug (FMPNP_DBG bit 2): s_memtime at the start of every evaluation of the team's first
     // problem and after its last, [grid][64] in the stamps buffer
     unsigned long long *ev_stamps =
         (kStamps && a.stamps != nullptr && (a.dbg & 4)) ? a.stamps + (size_t)blockIdx.x * 64 : nullptr;
+#if FMPNP_STAMPS
     if (stamps_on && (tid & 63) == 0) {
         for (int k = 0; k < NSTAMP; ++k) st.stamp_ph[tid >> 6][k] = 0;
         st.stamp_t[tid >> 6] = __builtin_amdgcn_s_memtime();
     }
+#endif
     constexpr bool kHelp = WPS == WPS_LATENCY && !TEAM && (VAR == VAR_GM_SPEC_H || VAR == VAR_NEAREST_SPEC_H ||
                                                            VAR == VAR_GM_H || VAR == VAR_NEAREST_H);
     if (helper) {
@@ -2551,9 +2571,11 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
         }
         problem_end(!TEAM, k, q.tl);
     }
+#if FMPNP_STAMPS
     if (stamps_on && (tid & 63) == 0)
         for (int k = 0; k < NSTAMP; ++k)
             a.stamps[((size_t)blockIdx.x * (NT / 64) + (tid >> 6)) * NSTAMP + k] = st.stamp_ph[tid >> 6][k];
+#endif
 }
 
 }  // namespace fmpnp

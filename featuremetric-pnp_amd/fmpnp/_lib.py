@@ -168,6 +168,15 @@ def _info_dict(info):
     return d
 
 
+from .build_id import kernel_name, source_digest  # noqa: E402,F401  (profile matching: bench.py)
+
+
+def library_digest():
+    """The source digest compiled into the loaded libfmpnp.so ("unknown" outside the Makefile)."""
+    info = load().fmpnp_build_info().decode()
+    return info.split("source_digest=", 1)[1].split(";")[0].strip() if "source_digest=" in info else "unknown"
+
+
 def last_launch():
     """Plan of this thread's last LM launch: geometry, build, kernel variant, helpers."""
     info = LaunchInfo()

@@ -101,7 +101,10 @@ class sparseFeaturePnP(nn.Module):
         want_trace = bool(track) or bool(self.verbose)
         (res,), traces = _rf.refine([prob], opts, trace=want_trace)
         self.last_result_ = res
-        self.status_ = res["status"]
+        # (FMPNP_STATUS_HELPER_WAIT is informational -- a first-evaluation helper workgroup was not
+        # resident in time and the main workgroup gathered itself, results unchanged -- so it is not
+        # part of the model's status: status_ == 0 means success, as for the reference)
+        self.status_ = res["status"] & ~_lib.STATUS_HELPER_WAIT
         if res["has_best"]:
             self.best_cost_ = torch.tensor(res["best_cost"], dtype=torch.float64)
             self.best_num_inliers_ = int(res["best_num_inliers"])

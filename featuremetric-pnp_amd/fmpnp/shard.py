@@ -68,6 +68,24 @@ def refine_sharded(make_problem, n_total, refine_fn, group=None):
     return out
 
 
+def device_accounting(device_ids):
+    """(n_gpus, ranks_per_device) of a job from the device identity each rank ran on: n_gpus
+    counts DISTINCT devices -- two ranks sharing one GPU (a gloo rehearsal on a one-GPU box) are
+    one GPU, never two."""
+    ids = [tuple(d) if isinstance(d, (list, tuple)) else d for d in device_ids]
+    n = len(set(ids))
+    return n, (len(ids) / n if n else 0.0)
+
+
+def gather_device_ids(my_id, group=None):
+    """Every rank's device identity (rank order)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return [my_id]
+    parts = [None] * dist.get_world_size(group)
+    dist.all_gather_object(parts, my_id, group=group)
+    return parts
+
+
 def max_over_ranks(x, device=None, group=None):
     """Max of a float over ranks (bench timing)."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:

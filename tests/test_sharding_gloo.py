@@ -131,16 +131,18 @@ def _bench(args, env_extra, timeout=240):
 def test_bench_gpus_n_starts_n_ranks():
     """`python bench.py --gpus 2` (the driver's form, no launcher) starts two rank processes
     itself; each sees WORLD_SIZE 2 and takes its own block of queries (dry run: no GPU)."""
-    rc, lines, err = _bench(["--gpus", "2", "--batch", "3"], {"FMPNP_BENCH_DRYRUN": "1"})
+    rc, lines, err = _bench(["--gpus", "2", "--batch", "3"], {"FMPNP_BENCH_DRYRUN": "1", "FMPNP_BENCH_NDEV": "2"})
     assert rc == 0, err
     assert sorted(d["rank"] for d in lines) == [0, 1]
     assert all(d["world"] == 2 for d in lines)
+    assert sorted(d["device"] for d in lines) == [0, 1]
+    assert all(d["n_gpus"] == 2 and d["ranks_per_device"] == 1.0 for d in lines)
     by_rank = {d["rank"]: d["queries"] for d in lines}
     assert by_rank[0] + by_rank[1] == list(range(6))
 
 
 def test_bench_strong_form_splits_the_total():
-    rc, lines, err = _bench(["--gpus", "2", "--global-batch", "5"], {"FMPNP_BENCH_DRYRUN": "1"})
+    rc, lines, err = _bench(["--gpus", "2", "--global-batch", "5"], {"FMPNP_BENCH_DRYRUN": "1", "FMPNP_BENCH_NDEV": "2"})
     assert rc == 0, err
     by_rank = {d["rank"]: d["queries"] for d in lines}
     assert by_rank[0] + by_rank[1] == list(range(5))
@@ -152,3 +154,85 @@ def test_bench_refuses_a_rank_count_other_than_gpus():
     rc, lines, err = _bench(["--gpus", "2"], {"WORLD_SIZE": "3", "RANK": "0", "FMPNP_BENCH_DRYRUN": "1"})
     assert rc == 2 and not lines
     assert "WORLD_SIZE" in err
+
+
+def test_bench_refuses_more_nccl_ranks_than_gpus():
+    """One process per GPU: with the nccl backend, more ranks than visible GPUs is an error (the
+    launcher used to map the surplus ranks onto one device silently and report them as GPUs)."""
+    rc, lines, err = _bench(["--gpus", "2"], {"FMPNP_BENCH_DRYRUN": "1", "FMPNP_BENCH_NDEV": "1"})
+    assert rc != 0 and not lines
+    assert "visible GPU" in err
+
+
+def test_bench_gloo_rehearsal_counts_one_gpu():
+    """The gloo rehearsal (two ranks on a one-GPU box) reports n_gpus 1, ranks 2."""
+    rc, lines, err = _bench(["--gpus", "2"], {"FMPNP_BENCH_DRYRUN": "1", "FMPNP_BENCH_NDEV": "1",
+                                              "FMPNP_BENCH_BACKEND": "gloo"})
+    assert rc == 0, err
+    assert sorted(d["rank"] for d in lines) == [0, 1]
+    assert all(d["n_gpus"] == 1 and d["ranks"] == 2 and d["ranks_per_device"] == 2.0 for d in lines)
+
+
+def test_device_accounting():
+    from fmpnp.shard import device_accounting
+    assert device_accounting([("h", 0, 3, 0)]) == (1, 1.0)
+    assert device_accounting([("h", 0, 3, 0), ("h", 0, 3, 0)]) == (1, 2.0)
+    assert device_accounting([("h", 0, 3, 0), ("h", 0, 4, 0), ("h", 0, 5, 0), ("h", 0, 6, 0)]) == (4, 1.0)
+    assert device_accounting([0, 1, 0, 1]) == (2, 2.0)
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_roofline_profile_must_match_kernel_and_build(tmp_path):
+    """bench.py's roofline takes bytes from a committed PMC profile only when the profile names
+    the kernel specialisation the launch ran AND was taken with the loaded library's sources;
+    otherwise it reports why and falls back to live gathered bytes."""
+    import json
+    bench = _bench_module()
+    (tmp_path / "profiles").mkdir()
+    k6 = "fmpnp::lm_kernel<float, 2, false, false, 6>"
+
+    def write(rnd, kernel, digest, nbytes=123):
+        with open(tmp_path / "profiles" / f"{rnd}_pmc_b128_easy.json", "w") as f:
+            json.dump({"kernel": f"void {kernel}(fmpnp::LaunchArgs)", "source_digest": digest,
+                       "hbm_bytes_per_launch": nbytes, "kernel_avg_ns": 1000.0}, f)
+
+    write("r03", k6, "aaaa", 100)
+    got = bench.load_traffic("b128_easy", k6, "aaaa", root=str(tmp_path))
+    assert got[0] == 100 and got[1] == k6 and got[4] is None
+    # another build of the same kernel: rejected with the reason
+    got = bench.load_traffic("b128_easy", k6, "bbbb", root=str(tmp_path))
+    assert got[0] is None and "taken with sources aaaa" in got[4]
+    # another specialisation (e.g. the ratio variant's profile under the plain tag): rejected
+    got = bench.load_traffic("b128_easy", "fmpnp::lm_kernel<float, 2, false, true, 6>", "aaaa", root=str(tmp_path))
+    assert got[0] is None and "is not the launch's" in got[4]
+    # a newer round's profile of another build does not hide an older matching one
+    write("r04", k6, "cccc", 200)
+    got = bench.load_traffic("b128_easy", k6, "aaaa", root=str(tmp_path))
+    assert got[0] == 100 and got[3].endswith("r03_pmc_b128_easy.json")
+    # a library built outside the Makefile has no digest: never matched
+    got = bench.load_traffic("b128_easy", k6, "unknown", root=str(tmp_path))
+    assert got[0] is None
+    # no profile at all
+    got = bench.load_traffic("b999_easy", k6, "aaaa", root=str(tmp_path))
+    assert got[0] is None and "no profiles" in got[4]
+
+
+def test_kernel_name_of_launch_plan():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "bid", os.path.join(ROOT, "featuremetric-pnp_amd", "fmpnp", "build_id.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    assert m.kernel_name(dict(dtype=0, build=2, team=0, ratio=0, variant=6)) == \
+        "fmpnp::lm_kernel<float, 2, false, false, 6>"
+    assert m.kernel_name(dict(dtype=1, build=4, team=1, ratio=1, variant=0)) == \
+        "fmpnp::lm_kernel<double, 4, true, true, 0>"
+    d = m.source_digest(ROOT)
+    assert len(d) == 16 and d == m.source_digest(ROOT)

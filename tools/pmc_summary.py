@@ -16,6 +16,19 @@ import json
 import os
 import sys
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def build_id():
+    """fmpnp/build_id.py loaded by path (no package import, no torch): the source digest bench.py
+    checks a profile against."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "fmpnp_build_id", os.path.join(ROOT, "featuremetric-pnp_amd", "fmpnp", "build_id.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
 
 def rows(pattern):
     out = []
@@ -60,6 +73,10 @@ def main():
         "hbm_bytes_per_launch": (None if fetch_kib is None or write_kib is None
                                  else int(2 * fetch_kib * 1024 + write_kib * 1024)),
         "correction": "FETCH_SIZE x2 (gfx950 wide-read halving), KiB -> bytes",
+        # the build the counters were taken with: bench.py uses the bytes only for this digest and
+        # this kernel specialisation (GIT_HEAD: set by the caller; the box has no git history)
+        "source_digest": build_id().source_digest(ROOT),
+        "git_head": os.environ.get("GIT_HEAD") or None,
         "all_kernels": [{k: r[k] for k in ("Name", "Calls", "AverageNs", "Percentage") if k in r} for r in stats],
     }
     with open(out, "w") as f:
