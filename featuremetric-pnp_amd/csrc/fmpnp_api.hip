@@ -72,6 +72,12 @@ int validate(const fmpnp_problem *probs, int n, const fmpnp_options *opt) {
 }
 
 int device_cus(int *ncu) {
+    // FMPNP_PLAN_CUS: plan for that many CUs without a device (host-side planner tests, the
+    // sanitizer run of tools/sanitize.sh); the occupancy query then falls back to one block per CU
+    if (const char *fc = getenv("FMPNP_PLAN_CUS")) {
+        *ncu = std::max(1, atoi(fc));
+        return 0;
+    }
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return (int)e;

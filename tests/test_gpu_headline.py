@@ -56,6 +56,7 @@ def check(res, tr, ores, otr, what):
     assert res["n_evals"] == ores["n_evals"] and res["n_steps"] == ores["n_steps"], what
     if tr is not None:
         np.testing.assert_array_equal(tr["n_supported"], otr["n_supported"], err_msg=what)
+        np.testing.assert_array_equal(tr["n_kept"], otr["n_kept"], err_msg=what)  # (the ratio test's kept set)
         np.testing.assert_allclose(tr["cost"], otr["cost"], rtol=1e-6, err_msg=what)
     assert res["best_num_inliers"] == ores["best_num_inliers"], what
     assert res["best_cost"] == pytest.approx(ores["best_cost"], rel=1e-6), what
