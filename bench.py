@@ -433,7 +433,7 @@ def run_legs(args, dev, probs, feats, inputs, opts, res_main, rf, _lib, synth):
     if "pipeline" in args.legs:
         out["end_to_end"] = pipeline_leg(dev, synth)
     if "pyramid1664" in args.legs:
-        out["pyramid_robotcar_1664"] = pyramid_leg(dev, rf, synth, _lib, stream)
+        out["pyramid_robotcar_1664"] = pyramid_legs(dev, rf, synth, _lib, stream)
     if ({"fixed1024", "no_memo", "bilinear"} & args.legs) and B < 1024 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         out.update(fixed_total_leg(args, dev, probs, feats, inputs, opts, rf, synth, stream, opt))
     if "cpu" in args.legs and int(os.environ.get("WORLD_SIZE", "1")) == 1:
@@ -496,18 +496,56 @@ def fixed_total_leg(args, dev, probs, feats, inputs, opts, rf, synth, stream, op
     return out
 
 
-def pyramid_leg(dev, rf, synth, _lib, stream, B=32):
+def pyramid_legs(dev, rf, synth, _lib, stream):
+    """The production pyramid at the largest (866) and the median (295) num_final_matches of
+    results/results_s2dhm/robotcar/summary.csv (column 5): the typical query and the worst one."""
+    out = pyramid_leg(dev, rf, synth, _lib, stream, N=866)
+    out["median_query_n295"] = pyramid_leg(dev, rf, synth, _lib, stream, N=295)
+    return out
+
+
+def pyramid_level_roofline(N, li, ms, gathers, C_level, root=ROOT):
+    """One pyramid level against the HBM roofline: HBM bytes per launch from the committed
+    rocprofv3 FETCH/WRITE summary (profiles/rNN_pmc_pyramid_n<N>.json, tools/gpu_profile_pyramid.sh)
+    taken with the loaded library's sources, else the live gathered bytes (gathers x 16 C + points)."""
+    from fmpnp import _lib
+    digest = _lib.library_digest()
+    for rnd in PROFILE_ROUNDS:
+        path = os.path.join("profiles", f"{rnd}_pmc_pyramid_n{N}.json")
+        try:
+            with open(os.path.join(root, path)) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if digest != "unknown" and d.get("source_digest") == digest:
+            lv = d["levels"][li]
+            b = lv["hbm_bytes_per_launch"]
+            return {"bound": "hbm", "achieved": round(b / (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK / 1e9,
+                    "unit": "GB/s", "frac": round(b / (ms / 1e3) / HBM_PEAK, 4), "traffic": b,
+                    "source": f"{path} (rocprofv3 {lv['kernel_avg_ns'] / 1e6:.4f} ms, {lv['kernel']})"}
+    b = gathers * 16 * C_level + 32 * N * 24
+    return {"bound": "hbm", "achieved": round(b / (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": round(b / (ms / 1e3) / HBM_PEAK, 4), "traffic": None,
+            "source": "LIVE gathered bytes (texel gathers x 16C + fp64 points): no committed PMC profile of this build"}
+
+
+def pyramid_leg(dev, rf, synth, _lib, stream, B=32, N=866):
     """The reference's production refinement: RobotCar hypercolumns of C = 1664 channels
-    (network.gin:18) at 256x256 for a 1024x1024 image, 866 points per query (the largest
-    num_final_matches of results/results_s2dhm/robotcar/summary.csv), Geman-McClure, 50 iterations
-    per level over the channel pyramid of input_configs/default_robotcar.gin:75
-    [(640,1664), (128,640), (0,128)] (multilevel_optimization, model.py:178-213).  B queries per
-    launch, one launch per level, each level starting from the previous level's poses."""
+    (network.gin:18) at 256x256 for a 1024x1024 image, N points per query (866: the largest
+    num_final_matches of results/results_s2dhm/robotcar/summary.csv; 295: its median),
+    Geman-McClure, 50 iterations per level over the channel pyramid of
+    input_configs/default_robotcar.gin:75 [(640,1664), (128,640), (0,128)] (multilevel_optimization,
+    model.py:178-213).  B queries per launch, one launch per level, each level starting from the
+    previous level's poses.  The planner's workgroups per query (G, each level's `launch`): 32 queries
+    leave 224 of the 256 CUs idle; a query of more than eight 64-point blocks (N = 866: 14) is spread
+    over G = 8 workgroups -- the fastest of G = 1, 2, 4, 8 measured at N = 866
+    (profiles/r03_pyramid1664_g_sweep.txt) --, one of at most eight (N = 295: 5 blocks) keeps G = 1,
+    where a member's exchange costs more than its share of the evaluation saves (fmpnp_api.hip)."""
     levels = [(640, 1664), (128, 640), (0, 128)]
     torch.cuda.synchronize()
     feats, frefs, inps = [], [], []
     for q in range(B):
-        inp = synth.problem_inputs(866, 1664, 256, 256, seed=20000 + q, device=dev, init="easy")
+        inp = synth.problem_inputs(N, 1664, 256, 256, seed=20000 + q, device=dev, init="easy")
         feats.append(rf.pack_features(inp.pop("fmap"), storage=torch.float32, device=dev))
         frefs.append(inp.pop("fref"))
         inps.append(inp)
@@ -515,22 +553,24 @@ def pyramid_leg(dev, rf, synth, _lib, stream, B=32):
     t = [i["t0"] for i in inps]
     opts = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32)
     per_level, total = [], 0.0
-    for cb, ce in levels:
+    for li, (cb, ce) in enumerate(levels):
         ps = [rf.make_problem(feats[q], frefs[q], inps[q]["pts3d"], inps[q]["K"], inps[q]["im_width"],
                               inps[q]["im_height"], R[q], t[q], c_begin=cb, c_end=ce) for q in range(B)]
         ms, res = time_launches(rf.AsyncBatch(ps, opts), 10, stream)
         total += ms
+        gathers = sum(r["texel_gathers"] for r in res)
         per_level.append({"channels": [cb, ce], "ms_per_launch": round(ms, 4), "launch": _lib.last_launch(),
                           "statuses": sorted({r["status"] for r in res}),
-                          "texel_gathers_per_point_eval": round(sum(r["texel_gathers"] for r in res) /
-                                                                max(1, 866 * sum(r["n_evals"] for r in res)), 4)})
+                          "texel_gathers_per_point_eval": round(gathers / max(1, N * sum(r["n_evals"] for r in res)),
+                                                                4),
+                          "roofline": pyramid_level_roofline(N, li, ms, gathers, ce - cb)})
         R = [r["R"] for r in res]
         t = [r["t"] for r in res]
     del feats, frefs
     torch.cuda.empty_cache()
-    return {"queries": B, "ms_per_batch": round(total, 4), "pose_refinements_per_s": round(B / (total / 1e3), 1),
-            "levels": per_level,
-            "workload": "C=1664 256x256 hypercolumns, 1024x1024 image, 866 points, GM, 50 iters per level, "
+    return {"queries": B, "points": N, "ms_per_batch": round(total, 4),
+            "pose_refinements_per_s": round(B / (total / 1e3), 1), "levels": per_level,
+            "workload": f"C=1664 256x256 hypercolumns, 1024x1024 image, {N} points, GM, 50 iters per level, "
                         "default_robotcar.gin:75 channel pyramid; sum of the three level launches"}
 
 
@@ -595,10 +635,43 @@ def pipeline_leg(dev, synth):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
-    return {"queries_per_s": round(nb * qb / best, 1), "ms_per_query": round(best / (nb * qb) * 1e3, 4),
-            "batches": nb, "batch": qb, "statuses": sorted({r["status"] for b in res for r in b}),
-            "note": "wall clock, host included: f-only pack and reference gather of every query (distinct maps) + "
-                    "one LM launch per batch, two streams"}
+    qps = nb * qb / best
+    out = {"queries_per_s": round(qps, 1), "ms_per_query": round(best / (nb * qb) * 1e3, 4),
+           "batches": nb, "batch": qb, "statuses": sorted({r["status"] for b in res for r in b}),
+           "note": "wall clock, host included: f-only pack and reference gather of every query (distinct maps) + "
+                   "one LM launch per batch, two streams"}
+    out["roofline"] = pipeline_roofline(qps)
+    return out
+
+
+def pipeline_roofline(qps, root=ROOT):
+    """The end-to-end leg against the HBM roofline: the HBM bytes per query of its kernels (the
+    f-only pack, the reference gather, the LM launches) from the committed rocprofv3 FETCH/WRITE
+    summary of the same workload (profiles/rNN_pmc_pipeline.json, tools/gpu_profile_pipeline.sh),
+    accepted only when taken with the loaded library's sources, times the wall-clock query rate."""
+    from fmpnp import _lib
+    digest = _lib.library_digest()
+    why = []
+    for rnd in PROFILE_ROUNDS:
+        path = os.path.join("profiles", f"{rnd}_pmc_pipeline.json")
+        try:
+            with open(os.path.join(root, path)) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if digest == "unknown" or d.get("source_digest") != digest:
+            why.append(f"{path}: taken with sources {d.get('source_digest')}, the loaded library is {digest}")
+            continue
+        bpq = d["hbm_bytes_per_query"]
+        ach = bpq * qps
+        return {"bound": "hbm", "achieved": round(ach / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK, 4), "traffic": int(bpq),
+                "traffic_unit": "HBM bytes per query (FETCH_SIZE x2 + WRITE_SIZE)", "source": path,
+                "bytes_per_query_by_kernel": {k: int(v["hbm_bytes_per_query"]) for k, v in d["families"].items()},
+                "kernel_us_per_query": round(d["kernel_ns_per_query"] / 1e3, 2),
+                "kernel_bound_queries_per_s": round(1e9 / d["kernel_ns_per_query"], 1)}
+    return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": None, "traffic": None,
+            "source": "no committed PMC profile of this build (" + ("; ".join(why) or "none") + ")"}
 
 
 def cpu_info():

@@ -26,7 +26,7 @@ ABI_VERSION = 2
 BUILD_WIDE, BUILD_LATENCY, BUILD_THROUGHPUT = 1, 2, 4
 BUILD_NAMES = {BUILD_WIDE: "wide", BUILD_LATENCY: "latency", BUILD_THROUGHPUT: "throughput"}
 VARIANT_NAMES = ["NEAREST", "GM", "BILINEAR", "F_NEAREST", "F_GM", "BIL_DIRECT", "GM_SPEC", "NEAREST_SPEC",
-                 "GM_SPEC_H", "NEAREST_SPEC_H", "GM_H", "NEAREST_H"]
+                 "GM_SPEC_H", "NEAREST_SPEC_H", "GM_H", "NEAREST_H", "GM_SS", "NEAREST_SS"]
 ERRORS = {-1: "EINVAL", -2: "EALIGN", -3: "ENOMEM", -4: "ETOOBIG", -5: "ENODEV"}
 
 

@@ -259,6 +259,9 @@ int fmpnp_last_launch(int *teams, int *wgs_per_problem, int *grid, int *lds_byte
 #define FMPNP_VAR_NEAREST_SPEC_H 9
 #define FMPNP_VAR_GM_H 10
 #define FMPNP_VAR_NEAREST_H 11
+#define FMPNP_VAR_GM_SS 12         /* GM_SPEC with the steady-state gather helpers: one helper workgroup
+                                      per problem gathers the predicted next texels every evaluation */
+#define FMPNP_VAR_NEAREST_SS 13    /* ... and for any loss */
 
 typedef struct {
     int teams, wgs_per_problem, grid, lds_bytes;

@@ -320,3 +320,32 @@ def test_helpers_that_never_publish_change_nothing(monkeypatch):
     assert base["best_cost"] == res["best_cost"] and base["texel_gathers"] == res["texel_gathers"]
     np.testing.assert_array_equal(tb["cost"], tr["cost"])
     np.testing.assert_array_equal(tb["n_supported"], tr["n_supported"])
+
+
+@pytest.mark.parametrize("B,init,ratio,loss", [(128, "easy", None, "gm"), (128, "hard", None, "gm"),
+                                               (1, "easy", None, "gm"), (128, "easy", 0.8, "gm"),
+                                               (16, "hard", 0.8, "gm"), (128, "easy", None, "cauchy")])
+def test_steady_helpers_change_nothing(B, init, ratio, loss, monkeypatch):
+    """The opt-in steady-state gather helpers (FMPNP_SS=1, VAR_GM_SS: one helper workgroup per
+    query predicts and gathers the next evaluation's texels on an idle CU; =2: they only prefetch)
+    move work, never a result: poses, costs, the schedule and the per-evaluation support are
+    bit-identical to the speculating variant, over repeated launches (the hand-off's tags are
+    launch-unique)."""
+    probs = [packed_problem(synth.problem_inputs(512, 256, 240, 320, seed=q, device=DEV, init=init))
+             for q in range(B)]
+    code, var = (_lib.GEMAN_MCCLURE, "GM") if loss == "gm" else (_lib.CAUCHY, "NEAREST")
+    o = rf.make_options(ITERS, 0.01, code, ratio_threshold=ratio, dtype=_lib.F32)
+    monkeypatch.delenv("FMPNP_SS", raising=False)
+    base, tb = rf.refine(probs, o, trace=True)
+    assert _lib.last_launch()["variant_name"] in (var + "_SPEC", var + "_SPEC_H")
+    for mode in ("1", "2", "1"):
+        monkeypatch.setenv("FMPNP_SS", mode)
+        res, tr = rf.refine(probs, o, trace=True)
+        assert _lib.last_launch()["variant_name"] == var + "_SS"
+        for q in range(B):
+            assert np.array_equal(res[q]["R"], base[q]["R"]) and np.array_equal(res[q]["t"], base[q]["t"]), q
+            assert res[q]["best_cost"] == base[q]["best_cost"] and res[q]["n_evals"] == base[q]["n_evals"], q
+            assert res[q]["status"] & ~_lib.STATUS_HELPER_WAIT == 0
+            np.testing.assert_array_equal(tr[q]["cost"], tb[q]["cost"])
+            np.testing.assert_array_equal(tr[q]["n_supported"], tb[q]["n_supported"])
+            np.testing.assert_array_equal(tr[q]["n_kept"], tb[q]["n_kept"])

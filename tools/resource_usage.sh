@@ -13,7 +13,7 @@ for line in sys.stdin:
     m = re.search(r"\s(VGPRs|TotalSGPRs|ScratchSize \[bytes/lane\]|VGPRs Spill|SGPRs Spill|LDS Size \[bytes/block\]): (\d+)", line)
     if m and cur is not None: cur[m.group(1)] = int(m.group(2))
 for r in rows:
-    n = re.sub(r"_ZN5fmpnp9lm_kernelI(\w)Li(\d)ELb(\d)ELb(\d)ELi(\d)EEEvNS_10LaunchArgsE", r"lm<\1,wps\2,team\3,ratio\4,var\5>", r["name"])
+    n = re.sub(r"_ZN5fmpnp9lm_kernelI(\w)Li(\d)ELb(\d)ELb(\d)ELi(\d+)EEEvNS_10LaunchArgsE", r"lm<\1,wps\2,team\3,ratio\4,var\5>", r["name"])
     g = lambda k: r.get(k, 0)
     print("%-40s vgpr %4d sgpr %4d scratch %5d vspill %4d" % (n, g("VGPRs"), g("TotalSGPRs"), g("ScratchSize [bytes/lane]"), g("VGPRs Spill")))
 '
