@@ -616,35 +616,52 @@ def pack_legs(dev, _lib, synth):
     return out
 
 
+PIPE_WINDOW = 5  # texels around each point's initial texel that the end-to-end leg packs (fmpnp.pipeline window)
+
+
 def pipeline_leg(dev, synth):
     """End to end from CHW hypercolumns (fmpnp.pipeline.RefinePipeline): pack + reference
-    gather + LM per batch, preparation of batch i+1 on a second stream under batch i's LM."""
+    gather + LM per batch, preparation of batch i+1 on a second stream under batch i's LM.
+    The leg's number is the windowed f-only pack (radius PIPE_WINDOW; a query that leaves its
+    window is packed in full and refined again -- `refills`, bit-identical results either way,
+    tests/test_window_pack.py); `full_pack` is the same workload with every texel packed."""
     import fmpnp
     from fmpnp.pipeline import RefinePipeline
     nb, qb = 4, 64
     batches, img = synth.pipeline_queries(nb, qb, N_PTS, C, HF, WF, device=dev, seed0=5000)
-    pipe = RefinePipeline(img, storage=torch.float32, depth=2,
-                          model_kwargs=dict(n_iters=ITERS, loss_fn=fmpnp.geman_mcclure_loss, lambda_=0.01,
-                                            ratio_threshold=None))
-    pipe.run(batches)  # sizes the slab ring
-    best = None
-    for _ in range(3):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        res = pipe.run(batches)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        best = dt if best is None else min(best, dt)
-    qps = nb * qb / best
+
+    def timed(window):
+        pipe = RefinePipeline(img, storage=torch.float32, depth=2, window=window,
+                              model_kwargs=dict(n_iters=ITERS, loss_fn=fmpnp.geman_mcclure_loss, lambda_=0.01,
+                                                ratio_threshold=None))
+        pipe.run(batches)  # sizes the slab ring
+        best = None
+        pipe.refills = 0
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            res = pipe.run(batches)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        return nb * qb / best, best, res, pipe.refills
+
+    qps, best, res, refills = timed(PIPE_WINDOW)
+    fqps, fbest, fres, _ = timed(None)
+    same = all(np.array_equal(a["R"], b["R"]) and np.array_equal(a["t"], b["t"]) and a["best_cost"] == b["best_cost"]
+               for x, y in zip(res, fres) for a, b in zip(x, y))
     out = {"queries_per_s": round(qps, 1), "ms_per_query": round(best / (nb * qb) * 1e3, 4),
            "batches": nb, "batch": qb, "statuses": sorted({r["status"] for b in res for r in b}),
-           "note": "wall clock, host included: f-only pack and reference gather of every query (distinct maps) + "
-                   "one LM launch per batch, two streams"}
-    out["roofline"] = pipeline_roofline(qps)
+           "window": PIPE_WINDOW, "refills_in_3_runs": refills, "identical_to_full_pack": same,
+           "note": "wall clock, host included: windowed f-only pack and reference gather of every query (distinct "
+                   "maps) + one LM launch per batch, two streams"}
+    out["roofline"] = pipeline_roofline(qps, PIPE_WINDOW)
+    out["full_pack"] = {"queries_per_s": round(fqps, 1), "ms_per_query": round(fbest / (nb * qb) * 1e3, 4),
+                        "roofline": pipeline_roofline(fqps, None)}
     return out
 
 
-def pipeline_roofline(qps, root=ROOT):
+def pipeline_roofline(qps, window=None, root=ROOT):
     """The end-to-end leg against the HBM roofline: the HBM bytes per query of its kernels (the
     f-only pack, the reference gather, the LM launches) from the committed rocprofv3 FETCH/WRITE
     summary of the same workload (profiles/rNN_pmc_pipeline.json, tools/gpu_profile_pipeline.sh),
@@ -653,7 +670,7 @@ def pipeline_roofline(qps, root=ROOT):
     digest = _lib.library_digest()
     why = []
     for rnd in PROFILE_ROUNDS:
-        path = os.path.join("profiles", f"{rnd}_pmc_pipeline.json")
+        path = os.path.join("profiles", f"{rnd}_pmc_pipeline{'_w%d' % window if window else ''}.json")
         try:
             with open(os.path.join(root, path)) as f:
                 d = json.load(f)
@@ -661,6 +678,9 @@ def pipeline_roofline(qps, root=ROOT):
             continue
         if digest == "unknown" or d.get("source_digest") != digest:
             why.append(f"{path}: taken with sources {d.get('source_digest')}, the loaded library is {digest}")
+            continue
+        if d.get("window") != window:
+            why.append(f"{path}: window {d.get('window')}, the leg's is {window}")
             continue
         bpq = d["hbm_bytes_per_query"]
         ach = bpq * qps

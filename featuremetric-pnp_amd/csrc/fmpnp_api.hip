@@ -42,6 +42,8 @@ int validate_problem(const fmpnp_problem &p, int layout, int sampling) {
     if (p.c_begin < 0 || p.c_end < p.c_begin || p.c_end > p.cstride || p.c_end > p.ld_ref) return FMPNP_EINVAL;
     if (p.N > 0 && (!p.feat || !p.fref || !p.pts3d)) return FMPNP_EINVAL;
     if (layout == FMPNP_LAYOUT_F && (p.Hf >= 65536 || p.Wf >= 65536)) return FMPNP_ETOOBIG;
+    // a packed window (fmpnp_pack_features_f_window_batch) is read by the f-only layout's gathers only
+    if (p.window && layout != FMPNP_LAYOUT_F) return FMPNP_EINVAL;
     // bilinear cell keys pack (row + 1, column + 1) into 15 + 16 bits
     if (sampling == FMPNP_BILINEAR && (p.Hf >= 32768 || p.Wf >= 65535)) return FMPNP_ETOOBIG;
     // the packed map must hold 3*cstride per texel
@@ -157,7 +159,12 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
         G = std::max(1, std::min(G, P.nc_max));
     }
     G = std::min(G, MAX_G);
-    while (G < std::min(P.nc_max, MAX_G) && !fits(G)) ++G;
+    // packed windows: one workgroup per problem (a window miss stops the problem inside its
+    // workgroup, fmpnp_lm_impl.h eval_pass; a team would wait on the stopped member)
+    bool windows = false;
+    for (int i = 0; i < n; ++i) windows = windows || probs[i].window != nullptr;
+    if (windows) G = 1;
+    while (!windows && G < std::min(P.nc_max, MAX_G) && !fits(G)) ++G;
     if (!fits(G)) return FMPNP_ETOOBIG;
     P.G = G;
     P.mmax = ((P.nc_max + G - 1) / G) * CH;
@@ -369,6 +376,27 @@ int fmpnp_pack_features_batch(int n, const void *const *chw, void *const *out, c
         if (e != hipSuccess) return (int)e;
     }
     return 0;
+}
+
+int fmpnp_pack_features_f_window_batch(const fmpnp_problem *probs_dev, const fmpnp_problem *probs_host, int n,
+                                       const void *const *chw, int dtype_in, int radius, void *hip_stream) {
+    if (n < 0 || (n > 0 && (!probs_dev || !probs_host || !chw))) return FMPNP_EINVAL;
+    if ((dtype_in != FMPNP_F32 && dtype_in != FMPNP_F64) || radius < 2 || radius > 4096) return FMPNP_EINVAL;
+    int max_n = 0;
+    long max_hw = 0;
+    for (int i = 0; i < n; ++i) {  // every item checked before anything is launched
+        const fmpnp_problem &p = probs_host[i];
+        const int rc = validate_problem(p, FMPNP_LAYOUT_F, FMPNP_NEAREST);
+        if (rc) return rc;
+        if (!chw[i] || !p.feat || !p.window || p.c_begin != 0 || p.c_end <= 0 || p.cstride % 4 ||
+            (uintptr_t)p.feat % 16 || (p.N > 0 && !p.pts3d))
+            return FMPNP_EINVAL;
+        max_n = std::max(max_n, p.N);
+        max_hw = std::max(max_hw, (long)p.Hf * p.Wf);
+    }
+    if (n == 0) return 0;
+    return (int)launch_pack_f_window(probs_dev, probs_host, n, chw, dtype_in, radius, max_n, max_hw,
+                                     (hipStream_t)hip_stream);
 }
 
 int fmpnp_gather_reference_batch(int n, const void *const *ref_chw, const int *ref_shape,

@@ -145,6 +145,11 @@ hipError_t launch_gather_ref(const void *ref, int dtype_in, int C, int H, int W,
 // n f-only packs (FMPNP_LAYOUT_F, fp32 out) in ceil(n / 32) launches; shape[4i..] = C, H, W, cstride
 hipError_t launch_pack_f_batch(int n, const void *const *chw, void *const *out, const int *shape, int dtype_in,
                                hipStream_t stream);
+// windowed f-only packs of n problems (fmpnp_pack_features_f_window_batch): clear the window maps,
+// mark each point's initial texel neighbourhood, pack the marked texels
+hipError_t launch_pack_f_window(const fmpnp_problem *probs_dev, const fmpnp_problem *probs_host, int n,
+                                const void *const *chw, int dtype_in, int radius, int max_n, long max_hw,
+                                hipStream_t stream);
 // n gathers in ceil(n / 32) launches (item table in the kernel arguments); err: [n] device flags
 hipError_t launch_gather_ref_batch(int n, const void *const *ref, const int *ref_shape, const double *const *inl,
                                    const int *n_inl, int img0, int img1, void *const *out, const int *ld_out,

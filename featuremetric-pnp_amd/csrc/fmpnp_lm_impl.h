@@ -81,6 +81,7 @@ struct Ctx {
     const void *feat;
     const void *fref;
     const double *pts;
+    const unsigned char *win_ok;  // packed window: texels whose 3x3 neighbourhood is packed (NULL: all)
     double K[9];
     int p, N, Hf, Wf, cs, cb, ce, ld_ref, im_w, im_h, vec;
     float txpx, typx, pxtx, pypx;  // texels per image pixel, image pixels per texel (x, y)
@@ -165,6 +166,7 @@ struct LMState {
     LMScal sc[2];
     double rho_max;
     int abort_flag, sync_ok;
+    int win_miss;           // a gather left the packed window (with abort_flag: FMPNP_STATUS_WINDOW)
     int helper_absent;      // a first-evaluation helper never published: the other blocks skip the wait
 #if FMPNP_STAMPS
     unsigned long long tlb[NT / 64][16];  // debug timeline (FMPNP_DBG bit 4), flushed at problem end
@@ -438,6 +440,7 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
         c.feat = pb->feat;
         c.fref = pb->fref;
         c.pts = pb->pts3d;
+        c.win_ok = pb->window ? pb->window + (size_t)pb->Hf * pb->Wf : nullptr;
         c.N = pb->N;
         c.Hf = pb->Hf;
         c.Wf = pb->Wf;
@@ -476,6 +479,7 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
             sc.nan = 0;
         }
         st.abort_flag = 0;
+        st.win_miss = 0;
         st.helper_absent = 0;
     }
     __syncthreads();
@@ -513,7 +517,9 @@ __device__ __forceinline__ void problem_end(bool own_gathers, int k, unsigned lo
 #endif
     if (threadIdx.x == 0) {
         LMScal &sc = st.sc[k & 1];
-        if (st.abort_flag) {
+        if (st.abort_flag && st.win_miss) {
+            sc.status |= FMPNP_STATUS_WINDOW;  // (one workgroup per problem: nothing else to stop)
+        } else if (st.abort_flag) {
             st.c.dead = 1;
             sc.status |= FMPNP_STATUS_SYNC_TIMEOUT;
         }
@@ -1688,6 +1694,23 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
             }
         }
         unsigned long long m = __ballot(dirty);
+        if constexpr (FL) {
+            // packed window (fmpnp_pack_features_f_window_batch): every texel gathered must have its
+            // 3x3 neighbourhood packed; a miss stops the problem after this evaluation (abort_flag is
+            // read only after barriers) with FMPNP_STATUS_WINDOW, its result invalid
+            const unsigned char *wok = ufirst(st.c.win_ok);
+            if (wok != nullptr && m) {
+                const bool miss = ((m >> lane) & 1ull) && wok[off] == 0;
+                const unsigned long long mm = __ballot(miss);
+                if (mm) {
+                    m &= ~mm;  // (never read an unpacked texel)
+                    if (lane == 0) {
+                        st.win_miss = 1;
+                        st.abort_flag = 1;
+                    }
+                }
+            }
+        }
 #if FMPNP_STAMPS
         if ((q.dbg & 128) && q.cur_ev > 0) m = 0;  // (diagnostics build, FMPNP_DBG bit 7: no gathers after eval 0 -- WRONG results, timing floor only)
 #endif

@@ -13,6 +13,8 @@
 // forward() receives them -- parity runs only).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 #include <stdlib.h>
 
 #include "fmpnp.h"
@@ -562,6 +564,192 @@ hipError_t launch_pack_f_batch(int n, const void *const *chw, void *const *out, 
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------------------
+// Windowed f-only pack (fmpnp_pack_features_f_window_batch).  The refinement reads only the
+// 3x3 neighbourhoods of the texels its points visit, a few texels from where they start, so
+// three kernels replace the full copy:
+//   win_clear_kernel  zero both planes of every problem's window map ([2][Hf][Wf] bytes);
+//   win_mark_kernel   one thread per point: its texel at (R0, t0) (the LM's projection and
+//                     indexing_, fmpnp_lm_impl.h project_pc) -> plane 0 over the square of
+//                     radius r, plane 1 over radius r - 1 (texels whose 3x3 neighbourhood is packed);
+//   hwc_win_kernel    hwc_tile's 64-channel x 32-column tiles, skipping a tile whose 32 texels are
+//                     all unmarked (its 128-byte channel rows are never read) and storing only
+//                     the marked texels.
+// A point whose projection differs in rounding from the LM's lands at most one texel off: the
+// LM checks plane 1 itself at every gather, so a miss is caught there (FMPNP_STATUS_WINDOW).
+__global__ __launch_bounds__(PK_NT) void win_clear_kernel(const fmpnp_problem *__restrict__ pd) {
+    const fmpnp_problem &p = pd[blockIdx.y];
+    const long nb = 2L * p.Hf * p.Wf;
+    unsigned char *w = const_cast<unsigned char *>(p.window);
+    const long n16 = ((uintptr_t)w % 16) == 0 ? nb / 16 : 0;  // 16-byte stores, then the tail bytes
+    for (long e = (long)blockIdx.x * PK_NT + threadIdx.x; e < n16; e += (long)gridDim.x * PK_NT)
+        reinterpret_cast<uint4 *>(w)[e] = make_uint4(0u, 0u, 0u, 0u);
+    for (long e = 16 * n16 + (long)blockIdx.x * PK_NT + threadIdx.x; e < nb; e += (long)gridDim.x * PK_NT) w[e] = 0;
+}
+
+__global__ __launch_bounds__(PK_NT) void win_mark_kernel(const fmpnp_problem *__restrict__ pd, int r) {
+    const fmpnp_problem &p = pd[blockIdx.y];
+    const int i = blockIdx.x * PK_NT + threadIdx.x;
+    if (i >= p.N) return;
+    const double *X = p.pts3d + 3 * (size_t)i;
+    double P[3];
+    for (int a = 0; a < 3; ++a) P[a] = p.R0[3 * a] * X[0] + p.R0[3 * a + 1] * X[1] + p.R0[3 * a + 2] * X[2] + p.t0[a];
+    const double u0 = p.K[0] * P[0] + p.K[1] * P[1] + p.K[2] * P[2];
+    const double u1 = p.K[3] * P[0] + p.K[4] * P[1] + p.K[5] * P[2];
+    const double u2 = p.K[6] * P[0] + p.K[7] * P[1] + p.K[8] * P[2];
+    const double px = rint(u0 / u2) - 1.0, py = rint(u1 / u2) - 1.0;
+    if (!(px >= 0.0 && px < (double)p.im_width && py >= 0.0 && py < (double)p.im_height)) return;
+    const int row = (int)(((unsigned long long)py * (unsigned)p.Hf) / (unsigned)p.im_height);
+    const int col = (int)(((unsigned long long)px * (unsigned)p.Wf) / (unsigned)p.im_width);
+    unsigned char *w0 = const_cast<unsigned char *>(p.window), *w1 = w0 + (size_t)p.Hf * p.Wf;
+    for (int y = max(row - r, 0); y <= min(row + r, p.Hf - 1); ++y)
+        for (int x = max(col - r, 0); x <= min(col + r, p.Wf - 1); ++x) {
+            w0[(size_t)y * p.Wf + x] = 1;
+            if (abs(y - row) < r && abs(x - col) < r) w1[(size_t)y * p.Wf + x] = 1;
+        }
+}
+
+struct WinItems {
+    const void *chw[HB_MAX];
+    int start[HB_MAX + 1];
+    int nct[HB_MAX], nxt[HB_MAX], vec[HB_MAX];
+    int n;
+    const fmpnp_problem *pd;  // the items' device descriptors (feat, window, sizes)
+};
+
+template <typename Tin, int HC_CT, int HC_XT>
+__global__ __launch_bounds__(HC_NT) void hwc_win_kernel(WinItems it) {
+    constexpr int HC_LD = HC_XT + 1;
+    __shared__ float tile[HC_CT * HC_LD];
+    __shared__ int flag[HC_XT];
+    int b = blockIdx.x;
+    int lo = 0, hi = it.n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (it.start[mid] <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    const fmpnp_problem &p = it.pd[lo];
+    const Tin *chw = reinterpret_cast<const Tin *>(it.chw[lo]);
+    const int C = p.c_end, H = p.Hf, W = p.Wf, cs = p.cstride, nct = it.nct[lo], nxt = it.nxt[lo];
+    float *out = reinterpret_cast<float *>(const_cast<void *>(p.feat));
+    b -= it.start[lo];
+    const int ct = b % nct;
+    b /= nct;
+    const int xt = b % nxt, y = b / nxt;
+    const int c0 = ct * HC_CT, x0 = xt * HC_XT;
+    (void)H;
+    int mine = 0;
+    if (threadIdx.x < HC_XT) {
+        const int x = x0 + threadIdx.x;
+        mine = x < W ? p.window[(size_t)y * W + x] : 0;
+        flag[threadIdx.x] = mine;
+    }
+    if (!__syncthreads_or(mine)) return;  // no marked texel in the tile: nothing read, nothing written
+    const bool full_x = x0 + HC_XT <= W;
+    constexpr int QPR = HC_XT / 4;
+    for (int i = threadIdx.x; i < HC_CT * QPR; i += HC_NT) {
+        const int cc = i / QPR, q = i - cc * QPR;
+        const int c = c0 + cc, x = x0 + 4 * q;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        if (c < C && (flag[4 * q] | flag[4 * q + 1] | flag[4 * q + 2] | flag[4 * q + 3])) {
+            const Tin *src = chw + ((size_t)c * p.Hf + y) * W + x;
+            if (it.vec[lo] && full_x) {
+                if constexpr (sizeof(Tin) == 4) {
+                    const float4 w = *reinterpret_cast<const float4 *>(src);
+                    v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
+                } else {
+                    const double2 w0 = *reinterpret_cast<const double2 *>(src);
+                    const double2 w1 = *reinterpret_cast<const double2 *>(src + 2);
+                    v[0] = (float)w0.x; v[1] = (float)w0.y; v[2] = (float)w1.x; v[3] = (float)w1.y;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (x + k < W) v[k] = (float)src[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tile[cc * HC_LD + 4 * q + k] = v[k];
+    }
+    __syncthreads();
+    constexpr int QPC = HC_CT / 4;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    for (int i = threadIdx.x; i < HC_XT * QPC; i += HC_NT) {
+        const int xx = i / QPC, cq = i - xx * QPC;
+        const int x = x0 + xx, c = c0 + 4 * cq;
+        if (x < W && c < cs && flag[xx]) {
+            f4 o;
+            o.x = tile[(4 * cq + 0) * HC_LD + xx];
+            o.y = tile[(4 * cq + 1) * HC_LD + xx];
+            o.z = tile[(4 * cq + 2) * HC_LD + xx];
+            o.w = tile[(4 * cq + 3) * HC_LD + xx];
+            __builtin_nontemporal_store(o, reinterpret_cast<f4 *>(out + ((size_t)y * W + x) * cs + c));
+        }
+    }
+}
+
+template <int CT, int XT>
+static hipError_t pack_f_window_tiles(const fmpnp_problem *probs_dev, const fmpnp_problem *probs_host, int n,
+                                      const void *const *chw, int dtype_in, hipStream_t stream) {
+    for (int i0 = 0; i0 < n; i0 += HB_MAX) {
+        WinItems it{};
+        const int m = std::min(n - i0, HB_MAX);
+        long total = 0;
+        for (int j = 0; j < m; ++j) {
+            const fmpnp_problem &p = probs_host[i0 + j];
+            it.chw[j] = chw[i0 + j];
+            it.nct[j] = (p.cstride + CT - 1) / CT;
+            it.nxt[j] = (p.Wf + XT - 1) / XT;
+            const size_t es = dtype_in == FMPNP_F64 ? 8 : 4;
+            it.vec[j] = ((uintptr_t)chw[i0 + j] % 16 == 0) && ((size_t)p.Wf * es) % 16 == 0;
+            it.start[j] = (int)total;
+            total += (long)it.nct[j] * it.nxt[j] * p.Hf;
+            if (total >= (1L << 31)) return hipErrorInvalidValue;
+        }
+        it.start[m] = (int)total;
+        it.n = m;
+        it.pd = probs_dev + i0;
+        if (dtype_in == FMPNP_F32)
+            hipLaunchKernelGGL((hwc_win_kernel<float, CT, XT>), dim3((unsigned)total), dim3(HC_NT), 0, stream, it);
+        else
+            hipLaunchKernelGGL((hwc_win_kernel<double, CT, XT>), dim3((unsigned)total), dim3(HC_NT), 0, stream, it);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_pack_f_window(const fmpnp_problem *probs_dev, const fmpnp_problem *probs_host, int n,
+                                const void *const *chw, int dtype_in, int radius, int max_n, long max_hw,
+                                hipStream_t stream) {
+    const unsigned ny = (unsigned)n;
+    const unsigned cb = (unsigned)std::min<long>((2 * max_hw + 16L * PK_NT - 1) / (16L * PK_NT), 1024);
+    hipLaunchKernelGGL(win_clear_kernel, dim3(std::max(cb, 1u), ny), dim3(PK_NT), 0, stream, probs_dev);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (max_n > 0) {
+        hipLaunchKernelGGL(win_mark_kernel, dim3((unsigned)((max_n + PK_NT - 1) / PK_NT), ny), dim3(PK_NT), 0, stream,
+                           probs_dev, radius);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    // tile (channels x columns), FMPNP_PACK_W_TILE: 1: 64 x 64 (default), 0: 64 x 32, 2: 128 x 32, 3: 32 x 64,
+    // 4: 128 x 64, 5: 256 x 32, 6: 64 x 128.  End to end at radius 5 (tools/window_sweep.py, queries/s):
+    // 64 x 64 33.1-33.2 k, 128 x 32 32.3-33.4 k, 64 x 32 30.7 k, 32 x 64 29.9 k, 256 x 32 26.5 k,
+    // 128 x 64 25.5 k, 64 x 128 22.8 k (profiles/r04_window_tiles.txt)
+    static const int tile = [] { const char *e = getenv("FMPNP_PACK_W_TILE"); return e ? atoi(e) : 1; }();
+    switch (tile) {
+    case 1: return pack_f_window_tiles<64, 64>(probs_dev, probs_host, n, chw, dtype_in, stream);
+    case 2: return pack_f_window_tiles<128, 32>(probs_dev, probs_host, n, chw, dtype_in, stream);
+    case 3: return pack_f_window_tiles<32, 64>(probs_dev, probs_host, n, chw, dtype_in, stream);
+    case 4: return pack_f_window_tiles<128, 64>(probs_dev, probs_host, n, chw, dtype_in, stream);
+    case 5: return pack_f_window_tiles<256, 32>(probs_dev, probs_host, n, chw, dtype_in, stream);
+    case 6: return pack_f_window_tiles<64, 128>(probs_dev, probs_host, n, chw, dtype_in, stream);
+    default: return pack_f_window_tiles<64, 32>(probs_dev, probs_host, n, chw, dtype_in, stream);
+    }
 }
 
 hipError_t launch_pack(const void *chw, const void *gx, const void *gy, int dtype_in, int C, int H, int W, void *out,

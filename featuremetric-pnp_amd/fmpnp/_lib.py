@@ -21,7 +21,8 @@ F32, F64 = 0, 1
 MODE_FORWARD, MODE_COMPUTE_COST = 0, 1
 STATUS_OK, STATUS_NO_SUPPORT, STATUS_NAN, STATUS_NO_SUPPORT_TRIAL, STATUS_SYNC_TIMEOUT = 0, 1, 2, 4, 8
 STATUS_HELPER_WAIT = 16  # informational: a first-evaluation helper did not publish in time (results unaffected)
-ABI_VERSION = 2
+STATUS_WINDOW = 32  # a point left its packed window (fmpnp_pack_features_f_window_batch): result invalid, re-run
+ABI_VERSION = 3
 # LM kernel builds and variants (fmpnp_launch_info)
 BUILD_WIDE, BUILD_LATENCY, BUILD_THROUGHPUT = 1, 2, 4
 BUILD_NAMES = {BUILD_WIDE: "wide", BUILD_LATENCY: "latency", BUILD_THROUGHPUT: "throughput"}
@@ -43,7 +44,8 @@ class Problem(ctypes.Structure):
                 ("Hf", ctypes.c_int), ("Wf", ctypes.c_int), ("cstride", ctypes.c_int), ("c_begin", ctypes.c_int),
                 ("c_end", ctypes.c_int), ("ld_ref", ctypes.c_int), ("N", ctypes.c_int),
                 ("im_width", ctypes.c_int), ("im_height", ctypes.c_int),
-                ("K", ctypes.c_double * 9), ("R0", ctypes.c_double * 9), ("t0", ctypes.c_double * 3)]
+                ("K", ctypes.c_double * 9), ("R0", ctypes.c_double * 9), ("t0", ctypes.c_double * 3),
+                ("window", ctypes.c_void_p)]
 
 
 class Result(ctypes.Structure):
@@ -70,7 +72,8 @@ class LaunchInfo(ctypes.Structure):
 EXPORTS = ["fmpnp_abi_version", "fmpnp_build_info", "fmpnp_device_check", "fmpnp_pack_features",
            "fmpnp_gather_reference", "fmpnp_gather_reference_async", "fmpnp_pack_features_batch", "fmpnp_pack_features_f",
            "fmpnp_gather_reference_batch", "fmpnp_workspace_size", "fmpnp_refine_batch_async", "fmpnp_refine_batch",
-           "fmpnp_last_launch", "fmpnp_debug_stamps", "fmpnp_plan", "fmpnp_last_launch_info"]
+           "fmpnp_last_launch", "fmpnp_debug_stamps", "fmpnp_plan", "fmpnp_last_launch_info",
+           "fmpnp_pack_features_f_window_batch"]
 
 _LIB = None
 
@@ -105,6 +108,8 @@ def load():
     L.fmpnp_pack_features_batch.restype = i
     L.fmpnp_gather_reference_batch.argtypes = [i, vp, vp, vp, vp, i, i, vp, vp, i, i, vp, vp]
     L.fmpnp_gather_reference_batch.restype = i
+    L.fmpnp_pack_features_f_window_batch.argtypes = [vp, vp, i, vp, i, i, vp]
+    L.fmpnp_pack_features_f_window_batch.restype = i
     L.fmpnp_point_costs.argtypes = [ctypes.POINTER(Problem), i, i, vp, vp, vp]
     L.fmpnp_point_costs.restype = i
     L.fmpnp_workspace_size.argtypes = [ctypes.POINTER(Problem), i, ctypes.POINTER(Options)]

@@ -18,7 +18,14 @@ stream and the LM launches on a `solve` stream, ordered by events:
   * the host runs at most `depth` batches ahead of the results it has collected.
 
 Results equal launching every batch alone (same kernels, same inputs; only the stream
-placement differs).  A query is (query_hc [C,H,W] or [1,C,H,W] device tensor,
+placement differs).
+
+`window=r` (the f-only layout) packs only the texels within r texels of each point's texel
+at the initial pose (fmpnp_pack_features_f_window_batch): the refinement reads only the 3x3
+neighbourhoods of the texels its points visit, a few texels from where they start.  The LM
+kernel checks every gather against the window and stops a problem that leaves it
+(FMPNP_STATUS_WINDOW); such queries are packed in full and refined again, so every result
+equals the fully packed pipeline's bit for bit.  A query is (query_hc [C,H,W] or [1,C,H,W] device tensor,
 reference_hc, prediction, K) with the reference's `Prediction` fields (points_3d,
 reference_inliers, matrix).
 """
@@ -43,7 +50,7 @@ def _streams(device):
 
 class RefinePipeline:
     def __init__(self, image_shape=None, storage=torch.float32, device=None, depth=2, model_kwargs=None,
-                 sampling="nearest", layout=None, wgs_per_problem=1):
+                 sampling="nearest", layout=None, wgs_per_problem=1, window=None):
         cfg = config.adapter_kwargs()
         self.image_shape = tuple(image_shape or cfg.get("image_shape", (1024, 1024)))
         self.storage = storage
@@ -67,6 +74,10 @@ class RefinePipeline:
         self.layout = layout or ("f" if f_ok else "fgrad")
         if self.layout == "f" and not f_ok:
             raise ValueError("layout 'f' needs fp32 storage and nearest sampling")
+        self.window = None if window is None else int(window)
+        if self.window is not None and (self.layout != "f" or self.window < 2):
+            raise ValueError("window needs the f-only layout and a radius >= 2")
+        self.refills = 0  # queries re-run with the full pack after leaving their window
         self.bound_options = _lib.Options.from_buffer_copy(self.options)
         self.bound_options.layout = _lib.LAYOUT_F if self.layout == "f" else _lib.LAYOUT_FGRAD
         self.prep, self.solve = _streams(self.device)
@@ -100,6 +111,8 @@ class RefinePipeline:
         Ws = np.array([m.shape[2] for m in qmaps], dtype=np.int64)
         css = (Cs + 3) // 4 * 4
         sizes = Hs * Ws * planes * css * es
+        if self.window is not None:  # [2][H][W] window bytes after each map
+            sizes = (sizes + _ALIGN - 1) // _ALIGN * _ALIGN + 2 * Hs * Ws
         starts = np.concatenate([[0], np.cumsum((sizes + _ALIGN - 1) // _ALIGN * _ALIGN)])
         inl = [np.asarray(q[2].reference_inliers, np.float64).reshape(-1, 2) for q in queries]
         pts = [np.asarray(q[2].points_3d, np.float64).reshape(-1, 3) for q in queries]
@@ -135,11 +148,12 @@ class RefinePipeline:
             vp = ctypes.c_void_p
             s = _lib.stream_ptr(dev)
             shape_arr = (ctypes.c_int * (4 * nq))(*np.stack([Cs, Hs, Ws, css], 1).reshape(-1).tolist())
-            rc = L.fmpnp_pack_features_batch(
-                nq, (vp * nq)(*[m.data_ptr() for m in qmaps]), (vp * nq)(*out_ptrs.tolist()), shape_arr,
-                _rf._dtype_code(q_dt), _rf._dtype_code(storage), 0, 0,
-                _lib.LAYOUT_F if self.layout == "f" else _lib.LAYOUT_FGRAD, s)                # :57, :61
-            _lib.check(rc, "fmpnp_pack_features_batch")
+            if self.window is None:
+                rc = L.fmpnp_pack_features_batch(
+                    nq, (vp * nq)(*[m.data_ptr() for m in qmaps]), (vp * nq)(*out_ptrs.tolist()), shape_arr,
+                    _rf._dtype_code(q_dt), _rf._dtype_code(storage), 0, 0,
+                    _lib.LAYOUT_F if self.layout == "f" else _lib.LAYOUT_FGRAD, s)            # :57, :61
+                _lib.check(rc, "fmpnp_pack_features_batch")
             rshape = (ctypes.c_int * (3 * nq))(*[v for m in rmaps for v in m.shape])
             base = dflat.data_ptr()
             rc = L.fmpnp_gather_reference_batch(
@@ -158,10 +172,49 @@ class RefinePipeline:
             desc["K"] = np.stack([np.asarray(q[3], np.float64).reshape(9) for q in queries])
             desc["R0"] = T[:, :3, :3].reshape(nq, 9)
             desc["t0"] = T[:, :3, 3]
+            if self.window is not None:
+                desc["window"] = out_ptrs + (Hs * Ws * css * es + _ALIGN - 1) // _ALIGN * _ALIGN
             batch = _rf.AsyncBatch.from_descriptors(desc, self.bound_options, dev, non_blocking=True)
+            if self.window is not None:  # the windowed pack reads the uploaded descriptors
+                rc = L.fmpnp_pack_features_f_window_batch(
+                    vp(batch.d_descs.data_ptr()), vp(batch.descs_np.ctypes.data), nq, (vp * nq)(*[m.data_ptr() for m in qmaps]),
+                    _rf._dtype_code(q_dt), self.window, s)                                     # :57, :61
+                _lib.check(rc, "fmpnp_pack_features_f_window_batch")
         # read on the prep stream (maps, converted copies) or the solve stream (the rest):
         # kept alive until the batch is collected
-        return batch, [qmaps, rmaps, fbuf, dflat], err
+        return batch, [qmaps, rmaps, fbuf, dflat, desc], err
+
+    def _refill(self, res, keep):
+        """Queries that left their packed window: pack their maps in full and refine them again
+        (same kernel, same descriptors but the window and the packed map)."""
+        bad = [i for i, r in enumerate(res) if r["status"] & _lib.STATUS_WINDOW]
+        if not bad:
+            return res
+        qmaps, desc = keep[0], keep[4]
+        dev = self.device
+        sub = desc[bad].copy()
+        sub["window"] = 0
+        bufs = []
+        L = _lib.load()
+        with torch.cuda.device(dev), torch.cuda.stream(self.solve):
+            for j, i in enumerate(bad):
+                m = qmaps[i]
+                C, H, W = m.shape
+                cs = int(sub["cstride"][j])
+                buf = torch.empty(H * W * cs, dtype=torch.float32, device=dev)
+                bufs.append(buf)
+                rc = L.fmpnp_pack_features_f(ctypes.c_void_p(m.data_ptr()), _rf._dtype_code(m.dtype), C, H, W,
+                                             ctypes.c_void_p(buf.data_ptr()), _lib.F32, cs, _lib.stream_ptr(dev))
+                _lib.check(rc, "fmpnp_pack_features_f")
+                sub["feat"][j] = buf.data_ptr()
+            b = _rf.AsyncBatch.from_descriptors(sub, self.bound_options, dev)
+            b.launch(_lib.stream_ptr(dev))
+            again = b.results()
+        self.refills += len(bad)
+        res = list(res)
+        for j, i in enumerate(bad):
+            res[i] = again[j]
+        return res
 
     def run(self, batches):
         """batches: iterable of lists of queries.  Returns a list (per batch) of result dicts
@@ -177,6 +230,8 @@ class RefinePipeline:
                 raise IndexError(f"batch {len(out)}: reference inliers of queries {bad} map outside the reference "
                                  "hypercolumn (optimize_feature_pnp.py:56 raises IndexError)")
             res = b.results()
+            if self.window is not None:
+                res = self._refill(res, entry[1])
             # as refine.refine(): a timed-out cross-workgroup exchange left poses unrefined
             if any(r["status"] & _lib.STATUS_SYNC_TIMEOUT for r in res):
                 raise _lib.FmpnpError(f"batch {len(out)}: cross-workgroup exchange timed out")

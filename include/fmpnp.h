@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define FMPNP_ABI_VERSION 2
+#define FMPNP_ABI_VERSION 3  /* 3: fmpnp_problem.window (windowed f-only packs) */
 
 /* robust losses, featurePnP/helpers/utils.py:15-78 */
 typedef enum {
@@ -81,6 +81,10 @@ typedef enum {
 #define FMPNP_STATUS_HELPER_WAIT 16      /* informational: a first-evaluation helper workgroup did not
                                             publish in time and the main workgroup gathered that block
                                             itself (results unaffected: same gather code) */
+#define FMPNP_STATUS_WINDOW 32           /* a point reached a texel whose 3x3 neighbourhood lies outside
+                                            the problem's packed window (fmpnp_problem.window): the
+                                            problem stopped early and its result is invalid -- pack its
+                                            map in full and refine it again (fmpnp.pipeline does) */
 
 /* argument errors (negative return codes) */
 #define FMPNP_EINVAL -1
@@ -128,6 +132,13 @@ typedef struct {
     int Hf, Wf, cstride, c_begin, c_end, ld_ref, N;
     int im_width, im_height;        /* image size in pixels (forward's im_width/im_height) */
     double K[9], R0[9], t0[3];      /* row-major */
+    const unsigned char *window;    /* NULL: feat holds every texel.  Else (FMPNP_LAYOUT_F, one workgroup
+                                       per problem) device [2][Hf][Wf] bytes written by
+                                       fmpnp_pack_features_f_window_batch: plane 0 = texel packed, plane 1 =
+                                       texel whose whole 3x3 neighbourhood is packed.  The LM kernel checks
+                                       plane 1 at every gather and stops the problem with
+                                       FMPNP_STATUS_WINDOW on a miss, so a result without that bit equals the
+                                       fully packed map's bit for bit. */
 } fmpnp_problem;
 
 typedef struct {
@@ -196,6 +207,17 @@ int fmpnp_gather_reference_async(const void *ref_chw, int dtype_in, int C, int H
 int fmpnp_pack_features_batch(int n, const void *const *chw, void *const *out, const int *shape, int dtype_in,
                               int dtype_out, int sobel_normalized, int sobel_replicate_pad, int layout,
                               void *hip_stream);
+/* Windowed f-only pack (FMPNP_LAYOUT_F) of n problems: only the texels within `radius` texels
+ * (Chebyshev distance, radius >= 2) of a point's texel at the problem's initial pose (R0, t0) are
+ * written to feat ([Hf][Wf][cstride] fp32, channels [c_end, cstride) zero), and window ([2][Hf][Wf]
+ * bytes, see fmpnp_problem.window) records which: plane 1 marks the texels within radius - 1.
+ * The reference's refinement reads only the 3x3 neighbourhoods of the texels its points visit
+ * (optimize_feature_pnp.py:57-61 packs all of them), so a radius a little above the points' motion
+ * in texels leaves most of the map unwritten and mostly unread.  probs_dev / probs_host: the same
+ * descriptors in device / host memory (feat and window set, c_begin = 0, C = c_end channels);
+ * chw[i]: map i, [c_end][Hf][Wf] of dtype_in.  Asynchronous on hip_stream. */
+int fmpnp_pack_features_f_window_batch(const fmpnp_problem *probs_dev, const fmpnp_problem *probs_host, int n,
+                                       const void *const *chw, int dtype_in, int radius, void *hip_stream);
 int fmpnp_gather_reference_batch(int n, const void *const *ref_chw, const int *ref_shape,
                                  const double *const *ref_inliers, const int *n_inliers, int img0, int img1,
                                  void *const *out, const int *ld_out, int dtype_in, int dtype_out, int *err_flags,

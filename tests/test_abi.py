@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     L = _lib.load()
     missing = [f for f in declared_functions() if not hasattr(L, f)]
     assert not missing, missing
-    assert L.fmpnp_abi_version() == _lib.ABI_VERSION == 2
+    assert L.fmpnp_abi_version() == _lib.ABI_VERSION == 3
     assert b"gfx950" in L.fmpnp_build_info()
 
 
@@ -123,3 +123,23 @@ def test_tail_sincos_matches_libm():
     subprocess.run(["make", "-s", "-C", pkg, "build/test_host_math"], check=True, timeout=300)
     r = subprocess.run([os.path.join(pkg, "build", "test_host_math")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_window_pack_rejects_bad_arguments_without_a_device():
+    """fmpnp_pack_features_f_window_batch validates every descriptor before launching: a radius
+    below 2, a missing window map or output, a channel slice not starting at 0."""
+    L = _lib.load()
+    vp = ctypes.c_void_p
+    p = _lib.Problem()
+    p.feat, p.fref, p.pts3d, p.window = 256, 256, 256, 4096
+    p.Hf, p.Wf, p.cstride, p.c_begin, p.c_end, p.ld_ref, p.N = 8, 8, 4, 0, 4, 4, 3
+    p.im_width, p.im_height = 32, 32
+    chw = (vp * 1)(4096)
+    assert L.fmpnp_pack_features_f_window_batch(256, ctypes.byref(p), 1, chw, 0, 1, None) == -1   # radius < 2
+    assert L.fmpnp_pack_features_f_window_batch(256, ctypes.byref(p), -1, chw, 0, 3, None) == -1  # n < 0
+    assert L.fmpnp_pack_features_f_window_batch(256, ctypes.byref(p), 1, chw, 5, 3, None) == -1   # dtype
+    for field, bad in (("window", None), ("feat", None), ("c_begin", 1), ("cstride", 6)):
+        q = _lib.Problem.from_buffer_copy(p)
+        setattr(q, field, bad)
+        assert L.fmpnp_pack_features_f_window_batch(256, ctypes.byref(q), 1, chw, 0, 3, None) == -1, field
+    assert L.fmpnp_pack_features_f_window_batch(256, ctypes.byref(p), 0, chw, 0, 3, None) == 0      # nothing to do

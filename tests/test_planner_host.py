@@ -18,7 +18,7 @@ def _cus(monkeypatch):
     monkeypatch.setenv("FMPNP_PLAN_CUS", "256")
 
 
-def descs(n, N=512, C=256, Hf=240, Wf=320, cb=0, ce=None, im=(1280, 960)):
+def descs(n, N=512, C=256, Hf=240, Wf=320, cb=0, ce=None, im=(1280, 960), window=False):
     arr = (_lib.Problem * max(n, 1))()
     cs = (C + 3) // 4 * 4
     for i in range(n):
@@ -28,6 +28,7 @@ def descs(n, N=512, C=256, Hf=240, Wf=320, cb=0, ce=None, im=(1280, 960)):
         p.im_width, p.im_height = im
         p.K[:] = [1000.0, 0, 640.0, 0, 1000.0, 480.0, 0, 0, 1]
         p.R0[:] = [1.0, 0, 0, 0, 1.0, 0, 0, 0, 1.0]
+        p.window = 0x4000 if window else None
     return arr
 
 
@@ -128,3 +129,16 @@ def test_validation_errors():
     d[0].feat = 0
     info = _lib.LaunchInfo()
     assert _lib.load().fmpnp_plan(d, 1, ctypes.byref(o), ctypes.byref(info)) == EINVAL
+
+
+def test_windowed_problems_plan_one_workgroup(monkeypatch):
+    """A packed window (fmpnp_problem.window) forces one workgroup per problem (a window miss
+    stops the problem inside its workgroup), and is refused outside the f-only layout."""
+    o = rf.make_options(**GM)
+    o.layout = _lib.LAYOUT_F
+    i = plan(1, o)
+    assert i["wgs_per_problem"] > 1  # (a single f-only problem spreads over CUs)
+    i = plan(1, o, window=True)
+    assert i["wgs_per_problem"] == 1 and i["team"] == 0
+    with pytest.raises(_lib.FmpnpError):
+        plan(1, rf.make_options(**GM), window=True)

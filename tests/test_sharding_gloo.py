@@ -224,6 +224,34 @@ def test_roofline_profile_must_match_kernel_and_build(tmp_path):
     assert got[0] is None and "no profiles" in got[4]
 
 
+def test_pipeline_roofline_profile_must_match_build_and_window(tmp_path, monkeypatch):
+    """The end-to-end leg's roofline takes bytes per query from a committed pipeline profile only
+    when it was taken with the loaded library's sources and the leg's pack window."""
+    import json
+    bench = _bench_module()
+    from fmpnp import _lib
+    monkeypatch.setattr(_lib, "library_digest", lambda: "aaaa")
+    (tmp_path / "profiles").mkdir()
+
+    def write(name, digest, window, bpq):
+        with open(tmp_path / "profiles" / name, "w") as f:
+            json.dump({"source_digest": digest, "window": window, "hbm_bytes_per_query": bpq,
+                       "kernel_ns_per_query": 20000.0, "families": {"pack": {"hbm_bytes_per_query": bpq}}}, f)
+
+    write("r04_pmc_pipeline_w5.json", "aaaa", 5, 1e8)
+    write("r04_pmc_pipeline.json", "aaaa", None, 2e8)
+    got = bench.pipeline_roofline(30000.0, 5, root=str(tmp_path))
+    assert got["traffic"] == 100000000 and got["frac"] == round(1e8 * 3e4 / bench.HBM_PEAK, 4)
+    got = bench.pipeline_roofline(30000.0, None, root=str(tmp_path))
+    assert got["traffic"] == 200000000 and got["source"].endswith("r04_pmc_pipeline.json")
+    write("r04_pmc_pipeline_w5.json", "aaaa", 6, 1e8)  # another radius under the name: refused
+    got = bench.pipeline_roofline(30000.0, 5, root=str(tmp_path))
+    assert got["frac"] is None and "window 6" in got["source"]
+    write("r04_pmc_pipeline_w5.json", "bbbb", 5, 1e8)  # another build: refused
+    got = bench.pipeline_roofline(30000.0, 5, root=str(tmp_path))
+    assert got["frac"] is None and "taken with sources bbbb" in got["source"]
+
+
 def test_kernel_name_of_launch_plan():
     import importlib.util
     spec = importlib.util.spec_from_file_location(

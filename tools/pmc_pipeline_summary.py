@@ -15,7 +15,7 @@ from pmc_summary import ROOT, build_id  # noqa: E402
 
 
 def family(name):
-    if "hwc" in name or "pack" in name:
+    if "hwc" in name or "pack" in name or "win_clear" in name or "win_mark" in name:
         return "pack"
     if "gather_ref" in name:
         return "gather_reference"
@@ -56,7 +56,7 @@ def main():
                      "hbm_bytes_per_query": b / queries, "dispatches_counted": [nf.get(fam, 0), nw.get(fam, 0)]}
     out = {"workload": "bench.py end_to_end: RefinePipeline, 4 batches x 64 cfg2 queries from CHW hypercolumns "
                        "(f-only pack + reference gather + LM), tools/pipeline_run.py",
-           "queries": queries, "families": fams,
+           "queries": queries, "window": int(os.environ.get("WINDOW", "0")) or None, "families": fams,
            "hbm_bytes_per_query": sum(v["hbm_bytes_per_query"] for v in fams.values()),
            "kernel_ns_per_query": sum(v["kernel_ns_per_query"] for v in fams.values()),
            "correction": "FETCH_SIZE x2 (gfx950 wide-read halving), KiB -> bytes",

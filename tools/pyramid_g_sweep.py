@@ -1,6 +1,7 @@
 """Workgroups per problem (G) on the RobotCar production pyramid (bench.py pyramid_leg's workload:
-C = 1664 at 256x256, 866 points, B queries, the default_robotcar.gin:75 channel levels): ms per
-level launch for each G.  Usage: python tools/pyramid_g_sweep.py [B] [G ...]"""
+C = 1664 at 256x256, N points (environment N, default 866; 295 the median query), B queries, the
+default_robotcar.gin:75 channel levels): ms per level launch for each G (0: the planner's choice).
+Usage: [N=295] python tools/pyramid_g_sweep.py [B] [G ...]"""
 import os
 import sys
 
@@ -16,7 +17,8 @@ dev = torch.device("cuda", 0)
 levels = [(640, 1664), (128, 640), (0, 128)]
 feats, frefs, inps = [], [], []
 for q in range(B):
-    inp = synth.problem_inputs(866, 1664, 256, 256, seed=20000 + q, device=dev, init="easy")
+    inp = synth.problem_inputs(int(os.environ.get("N", "866")), 1664, 256, 256, seed=20000 + q, device=dev,
+                               init="easy")
     feats.append(rf.pack_features(inp.pop("fmap"), storage=torch.float32, device=dev))
     frefs.append(inp.pop("fref"))
     inps.append(inp)
