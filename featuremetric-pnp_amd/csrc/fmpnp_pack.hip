@@ -423,6 +423,13 @@ static hipError_t pack_t(const void *chw, const void *gx, const void *gy, int C,
 // row), 512-byte texel segments out (32 lanes x 16 B of consecutive channels per column,
 // nt stores), i.e. 8C bytes per texel of HBM traffic and no gradient work.
 constexpr int HC_NT = 256;
+// the once-read CHW rows of the f-only packs: nontemporal loads (end to end with windowed packs
+// 33.7-33.9 k vs 33.2-33.5 k queries/s, profiles/r04_window_tiles.txt); -DFMPNP_PACK_NT_LOAD=0 for A/B
+#ifndef FMPNP_PACK_NT_LOAD
+#define FMPNP_PACK_NT_LOAD 1
+#endif
+constexpr bool kNtLoad = FMPNP_PACK_NT_LOAD != 0;
+typedef float nf4 __attribute__((ext_vector_type(4)));
 
 template <typename Tin, int HC_CT, int HC_XT>
 __device__ __forceinline__ void hwc_tile(const Tin *__restrict__ chw, int C, int H, int W, float *__restrict__ out,
@@ -442,7 +449,8 @@ __device__ __forceinline__ void hwc_tile(const Tin *__restrict__ chw, int C, int
             const Tin *src = chw + ((size_t)c * H + y) * W + x;
             if (vec_ok && full_x) {
                 if constexpr (sizeof(Tin) == 4) {
-                    const float4 w = *reinterpret_cast<const float4 *>(src);
+                    const nf4 w = kNtLoad ? __builtin_nontemporal_load(reinterpret_cast<const nf4 *>(src))
+                                          : *reinterpret_cast<const nf4 *>(src);
                     v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
                 } else {
                     const double2 w0 = *reinterpret_cast<const double2 *>(src);
@@ -529,15 +537,15 @@ static hipError_t hwc_t(const void *chw, int C, int H, int W, void *out, int cs,
     return hwc_ct<Tin, 64, 32>(chw, C, H, W, out, cs, stream);
 }
 
-template <typename Tin>
+template <typename Tin, int CT, int XT>
 static hipError_t hwc_batch_t(const HwcItems &it, int total, hipStream_t stream) {
-    hipLaunchKernelGGL((hwc_batch_kernel<Tin, 64, 32>), dim3((unsigned)total), dim3(HC_NT), 0, stream, it);
+    hipLaunchKernelGGL((hwc_batch_kernel<Tin, CT, XT>), dim3((unsigned)total), dim3(HC_NT), 0, stream, it);
     return hipGetLastError();
 }
 
-hipError_t launch_pack_f_batch(int n, const void *const *chw, void *const *out, const int *shape, int dtype_in,
-                               hipStream_t stream) {
-    constexpr int CT = 64, XT = 32;  // the single-map default (hwc_t)
+template <int CT, int XT>
+static hipError_t pack_f_batch_tiles(int n, const void *const *chw, void *const *out, const int *shape,
+                                     int dtype_in, hipStream_t stream) {
     for (int i0 = 0; i0 < n; i0 += HB_MAX) {
         HwcItems it{};
         const int m = n - i0 < HB_MAX ? n - i0 : HB_MAX;
@@ -559,11 +567,20 @@ hipError_t launch_pack_f_batch(int n, const void *const *chw, void *const *out, 
         }
         it.start[m] = (int)total;
         it.n = m;
-        const hipError_t e = dtype_in == FMPNP_F32 ? hwc_batch_t<float>(it, (int)total, stream)
-                                                   : hwc_batch_t<double>(it, (int)total, stream);
+        const hipError_t e = dtype_in == FMPNP_F32 ? hwc_batch_t<float, CT, XT>(it, (int)total, stream)
+                                                   : hwc_batch_t<double, CT, XT>(it, (int)total, stream);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t launch_pack_f_batch(int n, const void *const *chw, void *const *out, const int *shape, int dtype_in,
+                               hipStream_t stream) {
+    // tile (channels x columns), FMPNP_PACK_F_BTILE: 1: 64 x 64 (default), 0: 64 x 32 (end to end with
+    // the full pack: 25.2 k vs 24.2 k queries/s, profiles/r04_window_tiles.txt)
+    static const int tile = [] { const char *e = getenv("FMPNP_PACK_F_BTILE"); return e ? atoi(e) : 1; }();
+    return tile == 1 ? pack_f_batch_tiles<64, 64>(n, chw, out, shape, dtype_in, stream)
+                     : pack_f_batch_tiles<64, 32>(n, chw, out, shape, dtype_in, stream);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -611,10 +628,11 @@ __global__ __launch_bounds__(PK_NT) void win_mark_kernel(const fmpnp_problem *__
         }
 }
 
+constexpr int WB_MAX = 64;  // maps per windowed-pack launch (a pipeline batch of 64 queries in one grid)
 struct WinItems {
-    const void *chw[HB_MAX];
-    int start[HB_MAX + 1];
-    int nct[HB_MAX], nxt[HB_MAX], vec[HB_MAX];
+    const void *chw[WB_MAX];
+    int start[WB_MAX + 1];
+    int nct[WB_MAX], nxt[WB_MAX], vec[WB_MAX];
     int n;
     const fmpnp_problem *pd;  // the items' device descriptors (feat, window, sizes)
 };
@@ -658,7 +676,8 @@ __global__ __launch_bounds__(HC_NT) void hwc_win_kernel(WinItems it) {
             const Tin *src = chw + ((size_t)c * p.Hf + y) * W + x;
             if (it.vec[lo] && full_x) {
                 if constexpr (sizeof(Tin) == 4) {
-                    const float4 w = *reinterpret_cast<const float4 *>(src);
+                    const nf4 w = kNtLoad ? __builtin_nontemporal_load(reinterpret_cast<const nf4 *>(src))
+                                          : *reinterpret_cast<const nf4 *>(src);
                     v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
                 } else {
                     const double2 w0 = *reinterpret_cast<const double2 *>(src);
@@ -694,9 +713,9 @@ __global__ __launch_bounds__(HC_NT) void hwc_win_kernel(WinItems it) {
 template <int CT, int XT>
 static hipError_t pack_f_window_tiles(const fmpnp_problem *probs_dev, const fmpnp_problem *probs_host, int n,
                                       const void *const *chw, int dtype_in, hipStream_t stream) {
-    for (int i0 = 0; i0 < n; i0 += HB_MAX) {
+    for (int i0 = 0; i0 < n; i0 += WB_MAX) {
         WinItems it{};
-        const int m = std::min(n - i0, HB_MAX);
+        const int m = std::min(n - i0, WB_MAX);
         long total = 0;
         for (int j = 0; j < m; ++j) {
             const fmpnp_problem &p = probs_host[i0 + j];
