@@ -664,7 +664,40 @@ def pipeline_leg(dev, synth):
     out["roofline"] = pipeline_roofline(qps, PIPE_WINDOW)
     out["full_pack"] = {"queries_per_s": round(fqps, 1), "ms_per_query": round(fbest / (nb * qb) * 1e3, 4),
                         "roofline": pipeline_roofline(fqps, None)}
+    del batches
+    out["robotcar_1664"] = robotcar_pipeline_leg(dev, synth)
     return out
+
+
+def robotcar_pipeline_leg(dev, synth, nb=2, qb=32, N=866):
+    """End to end at the RobotCar production shape: CHW hypercolumns of C = 1664 at 256x256
+    (network.gin:18) for 1024x1024 images, N = 866 points (the largest num_final_matches of
+    results/results_s2dhm/robotcar/summary.csv), the channel pyramid of
+    input_configs/default_robotcar.gin:75 chained on the device (RefinePipeline levels), f-only
+    pack (full: 866 windows cover most of a 256x256 map) + reference gather + three LM launches
+    per batch of 32, preparation of the next batch under the current one's launches."""
+    import fmpnp
+    from fmpnp.pipeline import RefinePipeline
+    batches, img = synth.pipeline_queries(nb, qb, N, 1664, 256, 256, device=dev, seed0=7000)
+    pipe = RefinePipeline(img, storage=torch.float32, depth=2, levels=[(640, 1664), (128, 640), (0, 128)],
+                          model_kwargs=dict(n_iters=ITERS, loss_fn=fmpnp.geman_mcclure_loss, lambda_=0.01,
+                                            ratio_threshold=None))
+    pipe.run(batches)
+    best = None
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = pipe.run(batches)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    C, H, W = 1664, 256, 256
+    return {"queries_per_s": round(nb * qb / best, 1), "ms_per_query": round(best / (nb * qb) * 1e3, 4),
+            "batches": nb, "batch": qb, "points": N, "map": [C, H, W], "levels": [[640, 1664], [128, 640], [0, 128]],
+            "statuses": sorted({r["status"] for b in res for r in b}),
+            "pack_bytes_per_query": 8 * C * H * W,
+            "note": "wall clock, host included; f-only pack (8C bytes per texel) + reference gather + 3 level "
+                    "launches per batch, levels chained on the device"}
 
 
 def pipeline_roofline(qps, window=None, root=ROOT):

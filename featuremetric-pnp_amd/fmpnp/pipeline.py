@@ -25,7 +25,12 @@ at the initial pose (fmpnp_pack_features_f_window_batch): the refinement reads o
 neighbourhoods of the texels its points visit, a few texels from where they start.  The LM
 kernel checks every gather against the window and stops a problem that leaves it
 (FMPNP_STATUS_WINDOW); such queries are packed in full and refined again, so every result
-equals the fully packed pipeline's bit for bit.  A query is (query_hc [C,H,W] or [1,C,H,W] device tensor,
+equals the fully packed pipeline's bit for bit.
+
+`levels=[(c_begin, c_end), ...]` runs multilevel_optimization's channel pyramid
+(featurePnP/model.py:178-213, e.g. input_configs/default_robotcar.gin:75) on each batch: one LM
+launch per level over channel slices of the same packed map, each level starting from the
+previous level's poses, copied result -> descriptor on the device (no host round trip).  A query is (query_hc [C,H,W] or [1,C,H,W] device tensor,
 reference_hc, prediction, K) with the reference's `Prediction` fields (points_3d,
 reference_inliers, matrix).
 """
@@ -42,6 +47,36 @@ _ALIGN = 256          # byte alignment of each packed map inside a slab
 _STREAMS = {}         # device index -> (prep, solve): shared so the allocator's per-stream pools are reused
 
 
+class _LevelChain:
+    """One batch's LM launches over the channel levels: level l > 0 takes its initial poses from
+    level l - 1's results (R, t -> R0, t0 of the device descriptors) on the launching stream."""
+
+    def __init__(self, batches):
+        self.levels = batches
+        self.d_descs = batches[0].d_descs
+        self.d_res = batches[-1].d_res
+        self.d_ws = batches[0].d_ws
+
+    def launch(self, stream=None):
+        rs, ps = _rf.RESULT_DTYPE.itemsize, _rf.PROBLEM_DTYPE.itemsize
+        o_res, o_prob = _rf.RESULT_DTYPE.fields["R"][1], _rf.PROBLEM_DTYPE.fields["R0"][1]
+        for li, b in enumerate(self.levels):
+            if li:  # (R[9], t[3] and R0[9], t0[3] are contiguous: one 96-byte copy per problem)
+                prev = self.levels[li - 1].d_res.view(b.n, rs)
+                b.d_descs.view(b.n, ps)[:, o_prob:o_prob + 96].copy_(prev[:, o_res:o_res + 96], non_blocking=True)
+            b.launch(stream)
+
+    def tensors(self):
+        return [t for b in self.levels for t in (b.d_descs, b.d_res, b.d_ws)]
+
+    def results(self):
+        res = self.levels[-1].results()
+        for b in self.levels[:-1]:  # a timed-out exchange in any level left its poses unrefined
+            for r, e in zip(res, b.results()):
+                r["status"] |= e["status"] & _lib.STATUS_SYNC_TIMEOUT
+        return res
+
+
 def _streams(device):
     if device.index not in _STREAMS:
         _STREAMS[device.index] = (torch.cuda.Stream(device), torch.cuda.Stream(device))
@@ -50,7 +85,7 @@ def _streams(device):
 
 class RefinePipeline:
     def __init__(self, image_shape=None, storage=torch.float32, device=None, depth=2, model_kwargs=None,
-                 sampling="nearest", layout=None, wgs_per_problem=1, window=None):
+                 sampling="nearest", layout=None, wgs_per_problem=1, window=None, levels=None):
         cfg = config.adapter_kwargs()
         self.image_shape = tuple(image_shape or cfg.get("image_shape", (1024, 1024)))
         self.storage = storage
@@ -78,6 +113,9 @@ class RefinePipeline:
         if self.window is not None and (self.layout != "f" or self.window < 2):
             raise ValueError("window needs the f-only layout and a radius >= 2")
         self.refills = 0  # queries re-run with the full pack after leaving their window
+        self.levels = [tuple(int(c) for c in lv) for lv in levels] if levels else None
+        if self.levels and self.window is not None:
+            raise ValueError("channel levels run on fully packed maps (window=None)")
         self.bound_options = _lib.Options.from_buffer_copy(self.options)
         self.bound_options.layout = _lib.LAYOUT_F if self.layout == "f" else _lib.LAYOUT_FGRAD
         self.prep, self.solve = _streams(self.device)
@@ -174,7 +212,17 @@ class RefinePipeline:
             desc["t0"] = T[:, :3, 3]
             if self.window is not None:
                 desc["window"] = out_ptrs + (Hs * Ws * css * es + _ALIGN - 1) // _ALIGN * _ALIGN
-            batch = _rf.AsyncBatch.from_descriptors(desc, self.bound_options, dev, non_blocking=True)
+            if self.levels:
+                chain = []
+                for cb, ce in self.levels:
+                    if not (0 <= cb < ce <= int(Cs.min())):
+                        raise ValueError(f"channel level ({cb}, {ce}) outside the maps' {int(Cs.min())} channels")
+                    dl = desc.copy()
+                    dl["c_begin"], dl["c_end"] = cb, ce
+                    chain.append(_rf.AsyncBatch.from_descriptors(dl, self.bound_options, dev, non_blocking=True))
+                batch = _LevelChain(chain)
+            else:
+                batch = _rf.AsyncBatch.from_descriptors(desc, self.bound_options, dev, non_blocking=True)
             if self.window is not None:  # the windowed pack reads the uploaded descriptors
                 rc = L.fmpnp_pack_features_f_window_batch(
                     vp(batch.d_descs.data_ptr()), vp(batch.descs_np.ctypes.data), nq, (vp * nq)(*[m.data_ptr() for m in qmaps]),
@@ -249,7 +297,8 @@ class RefinePipeline:
             with torch.cuda.device(self.device), torch.cuda.stream(self.solve):
                 batch.launch(_lib.stream_ptr(self.device))
                 # buffers written on the prep stream and read on the solve stream
-                for t in (batch.d_descs, batch.d_res, batch.d_ws, err, self.slabs[k], keep[2], keep[3]):
+                extra = batch.tensors() if isinstance(batch, _LevelChain) else [batch.d_descs, batch.d_res, batch.d_ws]
+                for t in extra + [err, self.slabs[k], keep[2], keep[3]]:
                     t.record_stream(self.solve)
             done = torch.cuda.Event()
             done.record(self.solve)

@@ -135,3 +135,31 @@ def test_window_miss_stops_the_problem_with_its_status():
     for r, b in zip(res, base):
         if not r["status"] & _lib.STATUS_WINDOW:
             assert np.array_equal(r["R"], b["R"]) and r["best_cost"] == b["best_cost"]
+
+
+def test_pipeline_channel_levels_equal_level_by_level_runs():
+    """RefinePipeline(levels=...) (multilevel_optimization's channel pyramid, model.py:178-213,
+    poses chained on the device) equals running each level as its own pipeline pass, the next
+    level's initial pose taken from the previous level's results on the host."""
+    levels = [(32, 64), (8, 32), (0, 8)]
+    batches, img = synth.pipeline_queries(2, 5, N=128, C=64, Hf=48, Wf=64, device=DEV, seed0=1300)
+    kw = dict(n_iters=20, loss_fn=fmpnp.geman_mcclure_loss, lambda_=0.01, ratio_threshold=None)
+    chained = RefinePipeline(img, storage=torch.float32, depth=2, levels=levels, model_kwargs=kw).run(batches)
+    cur = batches
+    for lv in levels:
+        out = RefinePipeline(img, storage=torch.float32, depth=2, levels=[lv], model_kwargs=kw).run(cur)
+        nxt = []
+        for qs, rs in zip(cur, out):
+            row = []
+            for (a, b, p, k), r in zip(qs, rs):
+                T = np.eye(4)
+                T[:3, :3], T[:3, 3] = r["R"], r["t"]
+                row.append((a, b, p._replace(matrix=T), k))
+            nxt.append(row)
+        cur = nxt
+    for b0, b1 in zip(chained, out):
+        for r0, r1 in zip(b0, b1):
+            assert np.array_equal(r0["R"], r1["R"]) and np.array_equal(r0["t"], r1["t"])
+            assert r0["best_cost"] == r1["best_cost"] and r0["n_evals"] == r1["n_evals"]
+    with pytest.raises(ValueError):
+        RefinePipeline(img, storage=torch.float32, levels=levels, window=5, model_kwargs=kw)
