@@ -692,7 +692,9 @@ def robotcar_pipeline_leg(dev, synth, nb=2, qb=32, N=866):
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
     C, H, W = 1664, 256, 256
-    return {"queries_per_s": round(nb * qb / best, 1), "ms_per_query": round(best / (nb * qb) * 1e3, 4),
+    qps = nb * qb / best
+    return {"queries_per_s": round(qps, 1), "roofline": pipeline_roofline(qps, None, robotcar=True),
+            "ms_per_query": round(best / (nb * qb) * 1e3, 4),
             "batches": nb, "batch": qb, "points": N, "map": [C, H, W], "levels": [[640, 1664], [128, 640], [0, 128]],
             "statuses": sorted({r["status"] for b in res for r in b}),
             "pack_bytes_per_query": 8 * C * H * W,
@@ -700,7 +702,7 @@ def robotcar_pipeline_leg(dev, synth, nb=2, qb=32, N=866):
                     "launches per batch, levels chained on the device"}
 
 
-def pipeline_roofline(qps, window=None, root=ROOT):
+def pipeline_roofline(qps, window=None, root=ROOT, robotcar=False):
     """The end-to-end leg against the HBM roofline: the HBM bytes per query of its kernels (the
     f-only pack, the reference gather, the LM launches) from the committed rocprofv3 FETCH/WRITE
     summary of the same workload (profiles/rNN_pmc_pipeline.json, tools/gpu_profile_pipeline.sh),
@@ -709,7 +711,8 @@ def pipeline_roofline(qps, window=None, root=ROOT):
     digest = _lib.library_digest()
     why = []
     for rnd in PROFILE_ROUNDS:
-        path = os.path.join("profiles", f"{rnd}_pmc_pipeline{'_w%d' % window if window else ''}.json")
+        path = os.path.join("profiles", f"{rnd}_pmc_pipeline{'_w%d' % window if window else ''}"
+                                        f"{'_robotcar' if robotcar else ''}.json")
         try:
             with open(os.path.join(root, path)) as f:
                 d = json.load(f)

@@ -12,6 +12,7 @@ done
 [ -f "$P/sq/summary.txt" ] && cp "$P/sq/summary.txt" "profiles/${R}_sq_b128.txt"
 [ -f "$P/pipeline/summary.json" ] && cp "$P/pipeline/summary.json" "profiles/${R}_pmc_pipeline.json"
 [ -f "$P/pipeline_w5/summary.json" ] && cp "$P/pipeline_w5/summary.json" "profiles/${R}_pmc_pipeline_w5.json"
+[ -f "$P/pipeline_robotcar/summary.json" ] && cp "$P/pipeline_robotcar/summary.json" "profiles/${R}_pmc_pipeline_robotcar.json"
 for n in 866 295; do
   [ -f "$P/pyramid_n$n/summary.json" ] && cp "$P/pyramid_n$n/summary.json" "profiles/${R}_pmc_pyramid_n$n.json"
 done

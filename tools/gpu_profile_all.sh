@@ -18,6 +18,7 @@ b1024_easy_nomemo_bilinear|--no-memo --sampling bilinear" SQ=1 timeout -k 10 150
     > gpurun_out/prof_lm.log 2>&1 || { tail -20 gpurun_out/prof_lm.log; exit 1; }
 WINDOW=5 timeout -k 10 400 bash tools/gpu_profile_pipeline.sh > gpurun_out/prof_pipe_w5.log 2>&1 || exit 1
 timeout -k 10 400 bash tools/gpu_profile_pipeline.sh > gpurun_out/prof_pipe.log 2>&1 || exit 1
+ROBOTCAR=1 timeout -k 10 400 bash tools/gpu_profile_pipeline.sh > gpurun_out/prof_pipe_robotcar.log 2>&1 || exit 1
 timeout -k 10 400 bash tools/gpu_profile_pyramid.sh 866 > gpurun_out/prof_pyr866.log 2>&1 || exit 1
 timeout -k 10 400 bash tools/gpu_profile_pyramid.sh 295 > gpurun_out/prof_pyr295.log 2>&1 || exit 1
 cd /tmp && export TMPDIR=/tmp

@@ -6,7 +6,7 @@
 # WINDOW=r: the windowed packs of radius r (gpurun_out/prof/pipeline_w<r>/).
 set -o pipefail
 REPO="${GRAFT_REPO_ROOT:-$(pwd)}"
-D="$REPO/gpurun_out/prof/pipeline${WINDOW:+_w$WINDOW}"
+D="$REPO/gpurun_out/prof/pipeline${WINDOW:+_w$WINDOW}${ROBOTCAR:+_robotcar}"
 mkdir -p "$D"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/trace" -o run -- python3 "$REPO/tools/pipeline_run.py" 2 > "$D/run.log" 2>&1 || { tail -20 "$D/run.log"; exit 1; }

@@ -54,9 +54,13 @@ def main():
                      "fetch_bytes_per_query": 2 * fetch.get(fam, 0.0) * 1024 / queries,
                      "write_bytes_per_query": write.get(fam, 0.0) * 1024 / queries,
                      "hbm_bytes_per_query": b / queries, "dispatches_counted": [nf.get(fam, 0), nw.get(fam, 0)]}
-    out = {"workload": "bench.py end_to_end: RefinePipeline, 4 batches x 64 cfg2 queries from CHW hypercolumns "
+    robot = os.environ.get("ROBOTCAR") == "1"
+    out = {"workload": "bench.py end_to_end robotcar_1664: RefinePipeline with 3 channel levels, 2 batches x 32 "
+                       "queries of C = 1664 256x256 hypercolumns, N = 866 (tools/pipeline_run.py, ROBOTCAR=1)" if robot else
+                       "bench.py end_to_end: RefinePipeline, 4 batches x 64 cfg2 queries from CHW hypercolumns "
                        "(f-only pack + reference gather + LM), tools/pipeline_run.py",
-           "queries": queries, "window": int(os.environ.get("WINDOW", "0")) or None, "families": fams,
+           "queries": queries, "window": int(os.environ.get("WINDOW", "0")) or None, "robotcar": robot,
+           "families": fams,
            "hbm_bytes_per_query": sum(v["hbm_bytes_per_query"] for v in fams.values()),
            "kernel_ns_per_query": sum(v["kernel_ns_per_query"] for v in fams.values()),
            "correction": "FETCH_SIZE x2 (gfx950 wide-read halving), KiB -> bytes",
