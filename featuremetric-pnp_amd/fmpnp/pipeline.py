@@ -85,7 +85,7 @@ def _streams(device):
 
 class RefinePipeline:
     def __init__(self, image_shape=None, storage=torch.float32, device=None, depth=2, model_kwargs=None,
-                 sampling="nearest", layout=None, wgs_per_problem=1, window=None, levels=None):
+                 sampling="nearest", layout=None, wgs_per_problem=None, window=None, levels=None):
         cfg = config.adapter_kwargs()
         self.image_shape = tuple(image_shape or cfg.get("image_shape", (1024, 1024)))
         self.storage = storage
@@ -94,13 +94,16 @@ class RefinePipeline:
         kw = config.model_kwargs()
         kw.update(model_kwargs or {})
         loss_code, alpha = _losses.resolve(kw["loss_fn"])
-        # one workgroup per query by default, and no first-evaluation helpers: the LM launch then
-        # leaves the other CUs to the next batch's pack and gather on the prep stream, and no
-        # workgroup of a launch waits on another one (a helper) that those concurrent kernels
-        # could keep from being resident
+        # workgroups per query (None: per batch, as many as keep the LM launch on half of the CUs,
+        # the other half left to the next batch's pack and gather on the prep stream -- RobotCar
+        # C = 1664, 32 queries: G = 4 3.84 k queries/s against G = 1 3.34 k and the planner's G = 8
+        # 3.64 k, tools/robotcar_e2e.py), and no first-evaluation helpers: no workgroup of a launch
+        # waits on another one (a helper) that those concurrent kernels could keep from being resident
+        self.wgs = None if wgs_per_problem is None else int(wgs_per_problem)
+        self.ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
         self.options = _rf.make_options(kw["n_iters"], kw["lambda_"], loss_code, alpha, kw.get("ratio_threshold"),
                                         _rf._dtype_code(storage), sampling=sampling,
-                                        wgs_per_problem=int(wgs_per_problem), helpers=-1)
+                                        wgs_per_problem=self.wgs or 0, helpers=-1)
         self.sampling = sampling
         self.depth = max(1, int(depth))
         # "f" (f plane only, gradients formed in the LM gather) wherever it applies: fp32
@@ -121,6 +124,13 @@ class RefinePipeline:
         self.prep, self.solve = _streams(self.device)
         self.slabs = [None] * self.depth        # flat uint8 device buffers holding a batch's packed maps
         self.slab_free = [None] * self.depth    # event: the last launch that read the slab finished
+
+    def batch_options(self, nq):
+        """The launch options of a batch of nq queries: the bound options with the batch's
+        workgroups per query (a packed window takes one, fmpnp_api.hip make_plan)."""
+        o = _lib.Options.from_buffer_copy(self.bound_options)
+        o.wgs_per_problem = self.wgs if self.wgs is not None else max(1, (self.ncu // 2) // max(nq, 1))
+        return o
 
     def _slab(self, k, nbytes):
         """Slab k with room for nbytes, usable on the prep stream once its last reader finished."""
@@ -212,6 +222,7 @@ class RefinePipeline:
             desc["t0"] = T[:, :3, 3]
             if self.window is not None:
                 desc["window"] = out_ptrs + (Hs * Ws * css * es + _ALIGN - 1) // _ALIGN * _ALIGN
+            opts = self.batch_options(nq)
             if self.levels:
                 chain = []
                 for cb, ce in self.levels:
@@ -219,10 +230,10 @@ class RefinePipeline:
                         raise ValueError(f"channel level ({cb}, {ce}) outside the maps' {int(Cs.min())} channels")
                     dl = desc.copy()
                     dl["c_begin"], dl["c_end"] = cb, ce
-                    chain.append(_rf.AsyncBatch.from_descriptors(dl, self.bound_options, dev, non_blocking=True))
+                    chain.append(_rf.AsyncBatch.from_descriptors(dl, opts, dev, non_blocking=True))
                 batch = _LevelChain(chain)
             else:
-                batch = _rf.AsyncBatch.from_descriptors(desc, self.bound_options, dev, non_blocking=True)
+                batch = _rf.AsyncBatch.from_descriptors(desc, opts, dev, non_blocking=True)
             if self.window is not None:  # the windowed pack reads the uploaded descriptors
                 rc = L.fmpnp_pack_features_f_window_batch(
                     vp(batch.d_descs.data_ptr()), vp(batch.descs_np.ctypes.data), nq, (vp * nq)(*[m.data_ptr() for m in qmaps]),
@@ -255,7 +266,7 @@ class RefinePipeline:
                                              ctypes.c_void_p(buf.data_ptr()), _lib.F32, cs, _lib.stream_ptr(dev))
                 _lib.check(rc, "fmpnp_pack_features_f")
                 sub["feat"][j] = buf.data_ptr()
-            b = _rf.AsyncBatch.from_descriptors(sub, self.bound_options, dev)
+            b = _rf.AsyncBatch.from_descriptors(sub, self.batch_options(len(bad)), dev)
             b.launch(_lib.stream_ptr(dev))
             again = b.results()
         self.refills += len(bad)
