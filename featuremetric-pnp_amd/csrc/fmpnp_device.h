@@ -64,6 +64,31 @@ __device__ __forceinline__ double nanmax(double a, double b) {
     return (isnan(b) || b > a) ? (isnan(a) ? a : b) : a;
 }
 // max over the 64 lanes of a wave (order-free: exact)
+// wave maximum / minimum of non-NaN values (v_max_f64 / v_min_f64 semantics)
+__device__ __forceinline__ double wave_fmax(double v) {
+    v = fmax(v, dpp64<DPP_XOR1>(v));
+    v = fmax(v, dpp64<DPP_XOR2>(v));
+    v = fmax(v, dpp64<DPP_MIRROR8>(v));
+    v = fmax(v, dpp64<DPP_MIRROR16>(v));
+    double a = v, b = v;
+    swap16(a, b);
+    v = fmax(a, b);
+    a = v, b = v;
+    swap32(a, b);
+    return fmax(a, b);
+}
+__device__ __forceinline__ double wave_fmin(double v) {
+    v = fmin(v, dpp64<DPP_XOR1>(v));
+    v = fmin(v, dpp64<DPP_XOR2>(v));
+    v = fmin(v, dpp64<DPP_MIRROR8>(v));
+    v = fmin(v, dpp64<DPP_MIRROR16>(v));
+    double a = v, b = v;
+    swap16(a, b);
+    v = fmin(a, b);
+    a = v, b = v;
+    swap32(a, b);
+    return fmin(a, b);
+}
 __device__ __forceinline__ double wave_nanmax(double v) {
     v = nanmax(v, dpp64<DPP_XOR1>(v));
     v = nanmax(v, dpp64<DPP_XOR2>(v));

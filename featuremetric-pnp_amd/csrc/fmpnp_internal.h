@@ -78,7 +78,7 @@ constexpr int HREC = 7;
 #define FMPNP_STAMPS 0
 #endif
 // LDS head of the LM kernel (LMState, fmpnp_lm_impl.h): 2 KB in the product build
-__host__ __device__ constexpr int lds_fixed_bytes() { return FMPNP_STAMPS ? 4096 : 2304; }
+__host__ __device__ constexpr int lds_fixed_bytes() { return FMPNP_STAMPS ? 4608 : 2304; }
 // row stride (doubles) of the LM kernel's structure-of-arrays LDS records: odd, so the
 // writers of one point's fields fall in distinct banks (fmpnp_lm_impl.h lds_X / lds_rec)
 __host__ __device__ constexpr int lds_rs(int mmax) { return mmax + 1; }

@@ -168,6 +168,10 @@ struct LMState {
     int abort_flag, sync_ok;
     int win_miss;           // a gather left the packed window (with abort_flag: FMPNP_STATUS_WINDOW)
     int helper_absent;      // a first-evaluation helper never published: the other blocks skip the wait
+    // the ratio test with a guessed limit (at most 8 blocks): evaluation k's guess is rguess[k & 1];
+    // rstat[b] = max|rho| of block b's supported points (NaN-propagating)
+    double rguess[2];
+    double rstat[8];
 #if FMPNP_STAMPS
     unsigned long long tlb[NT / 64][16];  // debug timeline (FMPNP_DBG bit 4), flushed at problem end
 #endif
@@ -480,6 +484,7 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
         }
         st.abort_flag = 0;
         st.win_miss = 0;
+        st.rguess[0] = st.rguess[1] = INFINITY;  // (evaluation 0: no guess -- every supported point kept)
         st.helper_absent = 0;
     }
     __syncthreads();
@@ -1589,7 +1594,9 @@ __device__ __forceinline__ void spec_pass(const PC &q, int mmax, long long &ngat
 // SP: the variant can speculate (nearest sampling; bilinear never memoises).
 // ---------------------------------------------------------------------------
 // HS: the steady-state helpers fill the idle slots (ss_fill): every wave keeps two slots, none predicts.
-template <typename T, bool PIPE, bool FL, bool SP, bool HELP, bool HS = false>
+// R1: the ratio test with a guessed limit (ratio_guess_check): the block partials are formed in
+// this pass with the previous evaluation's limit, and each block's |rho| statistics are parked.
+template <typename T, bool PIPE, bool FL, bool SP, bool HELP, bool HS = false, bool R1 = false>
 __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ngath, const double pose[12]) {
     LMState &st = S();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1605,6 +1612,9 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
     const bool vec = ((((uintptr_t)feat) | ((uintptr_t)fref)) & 15) == 0 && cs % V == 0 && ld % V == 0 &&
                      cb % V == 0 && (ce - cb) % V == 0;
     const bool defer = q.use_ratio != 0;
+    // (the guessed-limit ratio test: one workgroup per problem of at most 8 blocks)
+    const bool r1 = R1 && defer && q.M <= 8 * 64;
+    const double rguess = r1 ? ufirst(st.rguess[q.cur_ev & 1]) : 0.0;
     // (a wave below spec_w0 keeps slot 0 and no predictions: the memoised path)
     // (HS with a.ss == 2, the prefetch-only helpers: the main speculates as the _SPEC variants do)
     const bool hs = HS && q.ss_fill;
@@ -1786,7 +1796,16 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
                 rec[6 * rs + i] = rho;
                 rec[7 * rs + i] = d1;
             }
-            if (sup) lmax = nanmax(lmax, fabs(rho));
+            if (R1 && r1) {
+                // the partials with the guessed limit, and the statistics that tell whether the
+                // true limit keeps the same points (ratio_guess_check)
+                const double a = fabs(rho);
+                contrib_block(q, mmax, blk, sup, sup && a < rguess, rho, d1, r, rs, Pc, dst_g);
+                const double bmax = wave_nanmax(sup ? a : -1.0);
+                if (lane == 0) st.rstat[blk] = bmax;
+            } else if (sup) {
+                lmax = nanmax(lmax, fabs(rho));
+            }
         } else {
             contrib_block(q, mmax, blk, sup, sup, rho, d1, r, rs, Pc, dst_g);
         }
@@ -1895,14 +1914,27 @@ __device__ __forceinline__ double eval_pass_bil(const PC &q, int mmax, long long
 
 // Second pass of the ratio test: the weights of points with |rho| >= max|rho| * thr
 // are zero (model.py:324-336); P is recomputed bit-identically from X.
-__device__ __forceinline__ void contrib_pass(const PC &q, int mmax) {
-    LMState &st = S();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__device__ __forceinline__ void contrib_block_at(const PC &q, int mmax, int blk, double limit, const double Re[9],
+                                                 const double te[3], double *dst_g) {
+    const int lane = threadIdx.x & 63;
     const double *X = lds_X(mmax);
     const double *rec = lds_rec(mmax);
     const int *tex = lds_tex(mmax, q.spec);
     const int rs = lds_rs(mmax);
-    const double limit = ufirst(st.rho_max) * st.c.ratio_thr;
+    const int i = blk * 64 + lane;
+    const bool valid = i < q.M;
+    const bool sup = valid && tex[i] >= 0;
+    double Pc[3] = {0.0, 0.0, 1.0};
+    if (sup) transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
+    const int ii = valid ? i : 0;
+    const double *r = rec + ii;  // rho, rho' (fields 6, 7: slot 0 only)
+    const double *rs6 = (q.spec && lds_slot(mmax, true)[ii]) ? lds_rec2(mmax) + ii : r;  // the sums' slot
+    const bool kept = sup && fabs(r[6 * rs]) < limit;
+    contrib_block(q, mmax, blk, sup, kept, r[6 * rs], r[7 * rs], rs6, rs, Pc, dst_g);
+}
+__device__ __forceinline__ void contrib_pass(const PC &q, int mmax, double limit) {
+    LMState &st = S();
+    const int wave = threadIdx.x >> 6;
     double *dst_g = q.part_g;
     if (q.G > 1) dst_g += (size_t)((ufirst((int)st.c.epoch) + 1) & 1) * q.nc_max * NV;
     double Re[9], te[3];
@@ -1911,18 +1943,53 @@ __device__ __forceinline__ void contrib_pass(const PC &q, int mmax) {
     for (int k = 0; k < 9; ++k) Re[k] = ufirst(pev[k]);
 #pragma unroll
     for (int k = 0; k < 3; ++k) te[k] = ufirst(pev[9 + k]);
-    for (int blk = wave; blk * 64 < q.M; blk += nwaves()) {
-        const int i = blk * 64 + lane;
-        const bool valid = i < q.M;
-        const bool sup = valid && tex[i] >= 0;
-        double Pc[3] = {0.0, 0.0, 1.0};
-        if (sup) transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
+    for (int blk = wave; blk * 64 < q.M; blk += nwaves()) contrib_block_at(q, mmax, blk, limit, Re, te, dst_g);
+}
+__device__ __forceinline__ void contrib_pass_block(const PC &q, int mmax, int blk, double limit) {
+    LMState &st = S();
+    double *dst_g = q.part_g;
+    if (q.G > 1) dst_g += (size_t)((ufirst((int)st.c.epoch) + 1) & 1) * q.nc_max * NV;
+    double Re[9], te[3];
+    const double *pev = st.Ret[q.cur_ev & 1];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Re[k] = ufirst(pev[k]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) te[k] = ufirst(pev[9 + k]);
+    contrib_block_at(q, mmax, blk, limit, Re, te, dst_g);
+}
+
+// The guessed-limit ratio test (every wave, after barrier 1; one workgroup per problem, at most 8
+// blocks -- one per wave).  The reference keeps a supported point iff |rho| < max|rho| * thr over
+// every supported point (model.py:120-129, 324-336): known only once every block's loss is.
+// eval_pass<R1> formed each block partial at once with the previous evaluation's limit g and parked
+// each block's max|rho|.  Here every wave takes the true limit L from those maxima and checks its own
+// block: where no supported point lies between g and L, the guess kept exactly the points L keeps
+// and the block partial is the one contrib_pass would form (same points, same code, same bits);
+// otherwise (a NaN |rho|, the first evaluation, a limit that crossed a point) the wave re-forms
+// its block with L.  The caller's barrier then publishes the re-formed partials.  Returns L.
+__device__ __forceinline__ double ratio_guess_check(const PC &q, int mmax, double guess, bool force,
+                                                    long long &nredo) {
+    LMState &st = S();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, M = q.M, nb = (M + 63) >> 6;
+    double b = lane < nb ? st.rstat[lane] : -1.0;
+    // (nb <= 8: lanes 0..7 of one row -- three DPP steps)
+    b = nanmax(b, dpp64<DPP_XOR1>(b));
+    b = nanmax(b, dpp64<DPP_XOR2>(b));
+    b = nanmax(b, dpp64<DPP_MIRROR8>(b));
+    const double limit = ufirst(b) * st.c.ratio_thr;
+    if (wave < nb) {
+        const int i = wave * 64 + lane;
+        const bool valid = i < M;
         const int ii = valid ? i : 0;
-        const double *r = rec + ii;  // rho, rho' (fields 6, 7: slot 0 only)
-        const double *rs6 = (q.spec && lds_slot(mmax, true)[ii]) ? lds_rec2(mmax) + ii : r;  // the sums' slot
-        const bool kept = sup && fabs(r[6 * rs]) < limit;
-        contrib_block(q, mmax, blk, sup, kept, r[6 * rs], r[7 * rs], rs6, rs, Pc, dst_g);
+        const double a = fabs(lds_rec(mmax)[6 * lds_rs(mmax) + ii]);
+        const bool sup = valid && lds_tex(mmax, q.spec)[ii] >= 0;
+        const bool miss = sup && ((a < limit) != (a < guess));  // (a NaN limit keeps nothing)
+        if (__ballot(miss) || force) {
+            ++nredo;
+            contrib_pass_block(q, mmax, wave, limit);
+        }
     }
+    return limit;
 }
 
 // ---------------------------------------------------------------------------
@@ -2721,6 +2788,8 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
         problem_begin(a.probs + p, p, mmax);
         // speculation: the nearest-sampling variants of the latency build.  The planner runs a
         // _SPEC variant exactly when it enables speculation (memoised), so the flag is a constant
+        // the ratio test with a guessed limit (ratio_guess_check): one workgroup per problem, nearest
+        constexpr bool kRatio1 = RATIO && !TEAM && VAR != VAR_BILINEAR;
         constexpr bool kSpec = kSpecBuild && WPS == WPS_LATENCY &&
                                (kSS || VAR == VAR_GM_SPEC || VAR == VAR_NEAREST_SPEC || VAR == VAR_GM_SPEC_H ||
                                 VAR == VAR_NEAREST_SPEC_H);
@@ -2780,17 +2849,30 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
             if constexpr (VAR == VAR_BILINEAR)
                 lmax = eval_pass_bil<T>(q, mmax, ngath);
             else
-                lmax = eval_pass<T, true, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST), kSpec, kHelp, kSS>(q, mmax,
-                                                                                                        ngath, pose);
-            if (q.use_ratio) {
+                lmax = eval_pass<T, true, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST), kSpec, kHelp, kSS, kRatio1>(
+                    q, mmax, ngath, pose);
+            // the ratio test: with one workgroup per problem of at most 8 blocks, the guessed limit
+            // (ratio_guess_check, after barrier 1); otherwise the two passes (exchange, contrib_pass)
+            const bool r1 = kRatio1 && q.use_ratio && q.M <= 8 * 64;
+            if (q.use_ratio && !r1) {
                 if (!ratio_exchange(lmax)) break;
-                contrib_pass(q, mmax);
+                contrib_pass(q, mmax, ufirst(st.rho_max) * st.c.ratio_thr);
             }
             const int wave = tid >> 6;
             constexpr bool FLV = VAR == VAR_F_GM || VAR == VAR_F_NEAREST;
             tl_stamp(q, 4);
             if (TEAM) team_arrive();
             else __syncthreads();
+            if (r1) {
+                // (FMPNP_DBG bit 5: every block re-formed -- the two-pass partials, for A/B tests;
+                // bit 6: the re-formed blocks counted in texel_gathers' high word)
+                long long nredo = 0;
+                const double limit = ratio_guess_check(q, mmax, ufirst(st.rguess[k & 1]), (q.dbg & 32) != 0, nredo);
+                if ((q.dbg & 64) && (tid & 63) == 0) ngath += nredo << 32;
+                tl_stamp(q, 15);  // (stamps build: the guess checked)
+                __syncthreads();  // (the re-formed partials)
+                if (tid == 0) st.rguess[(k + 1) & 1] = isnan(limit) ? INFINITY : limit;  // evaluation k + 1's guess
+            }
             tl_stamp(q, 5);
             // the tail (lm_tail): one workgroup per problem -- three waves, one role each; a team --
             // wave 0 after the exchange, every role

@@ -349,3 +349,32 @@ def test_steady_helpers_change_nothing(B, init, ratio, loss, monkeypatch):
             np.testing.assert_array_equal(tr[q]["cost"], tb[q]["cost"])
             np.testing.assert_array_equal(tr[q]["n_supported"], tb[q]["n_supported"])
             np.testing.assert_array_equal(tr[q]["n_kept"], tb[q]["n_kept"])
+
+
+@pytest.mark.parametrize("B,init,ratio", [(128, "easy", 0.8), (128, "hard", 0.8), (16, "easy", 0.5), (1, "hard", 0.8)])
+def test_ratio_guess_changes_nothing(B, init, ratio, monkeypatch):
+    """The ratio test with a guessed limit (fmpnp_lm_impl.h ratio_guess_check: block partials formed
+    in pass 1 with the previous evaluation's limit, re-formed only when the true limit crosses a
+    point) against the same kernel forced to re-form every evaluation (FMPNP_DBG bit 5, the
+    two-pass partials): poses, costs, support and kept counts bit-identical, and the guess right in
+    most evaluations (FMPNP_DBG bit 6 counts the re-forms)."""
+    probs = [packed_problem(synth.problem_inputs(512, 256, 240, 320, seed=q, device=DEV, init=init))
+             for q in range(B)]
+    o = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, ratio_threshold=ratio, dtype=_lib.F32)
+    monkeypatch.setenv("FMPNP_DBG", "96")  # every evaluation re-formed, counted
+    base, tb = rf.refine(probs, o, trace=True)
+    assert _lib.last_launch()["ratio"] == 1
+    monkeypatch.setenv("FMPNP_DBG", "64")  # the guess, re-forms counted
+    res, tr = rf.refine(probs, o, trace=True)
+    redo = sum(r["texel_gathers"] >> 32 for r in res)  # (re-formed 64-point blocks)
+    evals = sum(r["n_evals"] for r in res)
+    for q in range(B):
+        assert np.array_equal(res[q]["R"], base[q]["R"]) and np.array_equal(res[q]["t"], base[q]["t"]), q
+        assert res[q]["best_cost"] == base[q]["best_cost"] and res[q]["n_evals"] == base[q]["n_evals"], q
+        np.testing.assert_array_equal(tr[q]["cost"], tb[q]["cost"])
+        np.testing.assert_array_equal(tr[q]["n_supported"], tb[q]["n_supported"])
+        np.testing.assert_array_equal(tr[q]["n_kept"], tb[q]["n_kept"])
+        assert (res[q]["texel_gathers"] & 0xFFFFFFFF) == (base[q]["texel_gathers"] & 0xFFFFFFFF)
+    assert sum(r["texel_gathers"] >> 32 for r in base) == 8 * evals  # (forced: every block of every evaluation)
+    print(f"B={B} {init} ratio {ratio}: re-formed {redo} of {8 * evals} blocks")
+    assert redo < 4 * evals

@@ -13,7 +13,7 @@ import numpy as np, torch
 from fmpnp import _lib, refine as rf, synth
 
 SITES = ["start", "projected", "gathered", "contrib", "pre-barrier", "barrier1", "combined", "bookkeeping",
-         "solved", "pose stored", "spec done", "barrier2", "acc operands", "acc ldlt", "acc decided"]
+         "solved", "pose stored", "spec done", "barrier2", "acc operands", "acc ldlt", "acc decided", "ratio checked"]
 dev = torch.device("cuda", 0)
 probs = []
 for q in range(B):
@@ -46,6 +46,9 @@ for k, name in enumerate(SITES):
     if np.all(np.isnan(m[:, k])):
         continue
     print(name.ljust(13) + "".join("   ----  " if np.isnan(m[w, k]) else f"{m[w, k]:7.0f}  " for w in range(8)))
+med = np.nanmedian(rel, 0)
+print("median over workgroups (wave 0):", "  ".join(f"{SITES[k]} {med[0, k]:.0f}" for k in range(len(SITES))
+                                                      if not np.isnan(med[0, k])))
 # the slowest wave of each workgroup sets its barrier: mean over workgroups of the per-WG maximum
 for k in (3, 4, 10):
     v = rel[:, :, k]
