@@ -606,9 +606,12 @@ __global__ __launch_bounds__(PK_NT) void win_clear_kernel(const fmpnp_problem *_
     for (long e = 16 * n16 + (long)blockIdx.x * PK_NT + threadIdx.x; e < nb; e += (long)gridDim.x * PK_NT) w[e] = 0;
 }
 
+// one thread per (point, window row): 2r + 1 rows of the point's square (a thread per point with
+// (2r + 1)^2 serial stores left most CUs idle: 67 us per 64-query batch)
 __global__ __launch_bounds__(PK_NT) void win_mark_kernel(const fmpnp_problem *__restrict__ pd, int r) {
     const fmpnp_problem &p = pd[blockIdx.y];
-    const int i = blockIdx.x * PK_NT + threadIdx.x;
+    const int e = blockIdx.x * PK_NT + threadIdx.x, span = 2 * r + 1;
+    const int i = e / span, dy = e - i * span - r;
     if (i >= p.N) return;
     const double *X = p.pts3d + 3 * (size_t)i;
     double P[3];
@@ -621,11 +624,12 @@ __global__ __launch_bounds__(PK_NT) void win_mark_kernel(const fmpnp_problem *__
     const int row = (int)(((unsigned long long)py * (unsigned)p.Hf) / (unsigned)p.im_height);
     const int col = (int)(((unsigned long long)px * (unsigned)p.Wf) / (unsigned)p.im_width);
     unsigned char *w0 = const_cast<unsigned char *>(p.window), *w1 = w0 + (size_t)p.Hf * p.Wf;
-    for (int y = max(row - r, 0); y <= min(row + r, p.Hf - 1); ++y)
-        for (int x = max(col - r, 0); x <= min(col + r, p.Wf - 1); ++x) {
-            w0[(size_t)y * p.Wf + x] = 1;
-            if (abs(y - row) < r && abs(x - col) < r) w1[(size_t)y * p.Wf + x] = 1;
-        }
+    const int y = row + dy;
+    if (y < 0 || y >= p.Hf) return;
+    for (int x = max(col - r, 0); x <= min(col + r, p.Wf - 1); ++x) {
+        w0[(size_t)y * p.Wf + x] = 1;
+        if (abs(dy) < r && abs(x - col) < r) w1[(size_t)y * p.Wf + x] = 1;
+    }
 }
 
 constexpr int WB_MAX = 64;  // maps per windowed-pack launch (a pipeline batch of 64 queries in one grid)
@@ -750,7 +754,8 @@ hipError_t launch_pack_f_window(const fmpnp_problem *probs_dev, const fmpnp_prob
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (max_n > 0) {
-        hipLaunchKernelGGL(win_mark_kernel, dim3((unsigned)((max_n + PK_NT - 1) / PK_NT), ny), dim3(PK_NT), 0, stream,
+        const long nt = (long)max_n * (2 * radius + 1);
+        hipLaunchKernelGGL(win_mark_kernel, dim3((unsigned)((nt + PK_NT - 1) / PK_NT), ny), dim3(PK_NT), 0, stream,
                            probs_dev, radius);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
