@@ -1959,14 +1959,14 @@ __device__ __forceinline__ void contrib_pass_block(const PC &q, int mmax, int bl
 }
 
 // The guessed-limit ratio test (every wave, after barrier 1; one workgroup per problem, at most 8
-// blocks -- one per wave).  The reference keeps a supported point iff |rho| < max|rho| * thr over
+// blocks: one per wave in the latency build, two in the throughput build's four waves).  The reference keeps a supported point iff |rho| < max|rho| * thr over
 // every supported point (model.py:120-129, 324-336): known only once every block's loss is.
 // eval_pass<R1> formed each block partial at once with the previous evaluation's limit g and parked
-// each block's max|rho|.  Here every wave takes the true limit L from those maxima and checks its own
-// block: where no supported point lies between g and L, the guess kept exactly the points L keeps
-// and the block partial is the one contrib_pass would form (same points, same code, same bits);
-// otherwise (a NaN |rho|, the first evaluation, a limit that crossed a point) the wave re-forms
-// its block with L.  The caller's barrier then publishes the re-formed partials.  Returns L.
+// each block's max|rho|.  Here every wave takes the true limit L from those maxima and checks the
+// blocks it owns (eval_pass's blk = wave, wave + nwaves(), ...): where no supported point lies
+// between g and L, the guess kept exactly the points L keeps and the block partial is the one
+// contrib_pass would form (same points, same code, same bits); otherwise (a NaN |rho|, the first
+// evaluation, a limit that crossed a point) the wave re-forms that block with L.  The caller's barrier then publishes the re-formed partials.  Returns L.
 __device__ __forceinline__ double ratio_guess_check(const PC &q, int mmax, double guess, bool force,
                                                     long long &nredo) {
     LMState &st = S();
@@ -1977,8 +1977,8 @@ __device__ __forceinline__ double ratio_guess_check(const PC &q, int mmax, doubl
     b = nanmax(b, dpp64<DPP_XOR2>(b));
     b = nanmax(b, dpp64<DPP_MIRROR8>(b));
     const double limit = ufirst(b) * st.c.ratio_thr;
-    if (wave < nb) {
-        const int i = wave * 64 + lane;
+    for (int blk = wave; blk < nb; blk += nwaves()) {
+        const int i = blk * 64 + lane;
         const bool valid = i < M;
         const int ii = valid ? i : 0;
         const double a = fabs(lds_rec(mmax)[6 * lds_rs(mmax) + ii]);
@@ -1986,7 +1986,7 @@ __device__ __forceinline__ double ratio_guess_check(const PC &q, int mmax, doubl
         const bool miss = sup && ((a < limit) != (a < guess));  // (a NaN limit keeps nothing)
         if (__ballot(miss) || force) {
             ++nredo;
-            contrib_pass_block(q, mmax, wave, limit);
+            contrib_pass_block(q, mmax, blk, limit);
         }
     }
     return limit;

@@ -248,7 +248,8 @@ def _oracle_subset(qs, ratio):
 
 @pytest.mark.parametrize("B,ratio,build,variant", [(128, None, "latency", "GM_SPEC"),
                                                    (128, 0.8, "latency", "GM_SPEC"),
-                                                   (512, None, "throughput", "GM")])
+                                                   (512, None, "throughput", "GM"),
+                                                   (512, 0.8, "throughput", "GM")])
 def test_bench_launch_against_oracle(B, ratio, build, variant):
     """The headline launch (B = 128: lm_kernel<float, latency, !team, ratio, VAR_GM_SPEC>, grid 128,
     no first-evaluation helpers), its ratio-test form (input_configs/full_robotcar_08.gin:40), and
@@ -351,7 +352,8 @@ def test_steady_helpers_change_nothing(B, init, ratio, loss, monkeypatch):
             np.testing.assert_array_equal(tr[q]["n_kept"], tb[q]["n_kept"])
 
 
-@pytest.mark.parametrize("B,init,ratio", [(128, "easy", 0.8), (128, "hard", 0.8), (16, "easy", 0.5), (1, "hard", 0.8)])
+@pytest.mark.parametrize("B,init,ratio", [(128, "easy", 0.8), (128, "hard", 0.8), (16, "easy", 0.5), (1, "hard", 0.8),
+                                          (512, "easy", 0.8)])
 def test_ratio_guess_changes_nothing(B, init, ratio, monkeypatch):
     """The ratio test with a guessed limit (fmpnp_lm_impl.h ratio_guess_check: block partials formed
     in pass 1 with the previous evaluation's limit, re-formed only when the true limit crosses a
@@ -363,7 +365,7 @@ def test_ratio_guess_changes_nothing(B, init, ratio, monkeypatch):
     o = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, ratio_threshold=ratio, dtype=_lib.F32)
     monkeypatch.setenv("FMPNP_DBG", "96")  # every evaluation re-formed, counted
     base, tb = rf.refine(probs, o, trace=True)
-    assert _lib.last_launch()["ratio"] == 1
+    assert _lib.last_launch()["ratio"] == 1  # (B = 512: the throughput build, two blocks per wave)
     monkeypatch.setenv("FMPNP_DBG", "64")  # the guess, re-forms counted
     res, tr = rf.refine(probs, o, trace=True)
     redo = sum(r["texel_gathers"] >> 32 for r in res)  # (re-formed 64-point blocks)
