@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--legs", default="all", help="comma list of " + ",".join(LEGS) + ", or all / none")
     ap.add_argument("--cpu-sample", type=int, default=1024, help="problems in the C-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="side file for every leg's full record (the stdout line carries one summary per leg)")
     a = ap.parse_args()
     a.legs = set(LEGS) if a.legs == "all" else set() if a.legs == "none" else set(a.legs.split(","))
     if a.legs - set(LEGS):
@@ -85,6 +87,95 @@ def parse():
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+LINE_MAX_BYTES = 6000  # the driver keeps the tail of stdout: the line must fit it whole
+_HEAD_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "gn_iters_per_s", "roofline", "cpu_baseline", "statuses",
+              "rehearsal")
+_ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "avg_kernel_ms",
+              "rocprof_avg_kernel_ms", "reference_equivalent_GBps")
+_CONFIG_KEYS = ("workload", "points", "channels", "feature_map", "iters", "loss", "texel_storage", "init",
+                "ratio_threshold", "layout", "batch_per_gpu", "global_batch", "parallelism", "ranks")
+_MS_KEYS = ("ms_per_launch", "ms_per_refinement", "ms_per_call", "ms_per_batch", "ms_per_query", "ms")
+_RATE_KEYS = ("pose_refinements_per_s", "queries_per_s", "calls_per_s", "gn_iters_per_s", "GB_per_s")
+
+
+def write_detail(out, path):
+    """Every leg's full record (launch plans, byte rules, per-level rooflines, ...) as a side
+    file; returns {"path", "sha256", "bytes"} for the stdout line, or a reason it was not written."""
+    import hashlib
+    blob = json.dumps(out, indent=1, default=str).encode()
+    try:
+        d = os.path.dirname(path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        with open(path, "wb") as f:
+            f.write(blob)
+    except OSError as e:
+        return {"path": None, "error": str(e)}
+    return {"path": path, "sha256": hashlib.sha256(blob).hexdigest(), "bytes": len(blob)}
+
+
+def _leg_summary_compact(d):
+    """One leg -> {ms, rate, frac} (+ a bit-identity flag where the leg has one)."""
+    s = {}
+    for k in _MS_KEYS:
+        if isinstance(d.get(k), (int, float)):
+            s["ms"] = d[k]
+            break
+    for k in _RATE_KEYS:
+        if isinstance(d.get(k), (int, float)):
+            s["rate"] = d[k]
+            s["rate_unit"] = k
+            break
+    roof = d.get("roofline")
+    if isinstance(roof, dict) and roof.get("frac") is not None:
+        s["frac"] = roof["frac"]
+    elif isinstance(d.get("frac_of_peak"), (int, float)):
+        s["frac"] = d["frac_of_peak"]
+    for k in ("poses_bit_identical_to_headline", "identical_to_full_pack", "refills_in_3_runs", "within_1e-4"):
+        if k in d:
+            s[k] = d[k]
+    return s
+
+
+def compact_line(out, detail_ref):
+    """The driver's JSON line: the headline keys (metric, value, ..., roofline, cpu_baseline) and
+    ONE summary per leg; the legs' full records stay in the side file named by `detail`."""
+    line = {k: out[k] for k in _HEAD_KEYS if k in out}
+    if isinstance(line.get("config"), dict):
+        line["config"] = {k: line["config"][k] for k in _CONFIG_KEYS if k in line["config"]}
+    if isinstance(line.get("roofline"), dict):
+        r = line["roofline"]
+        line["roofline"] = {k: r[k] for k in _ROOF_KEYS if k in r}
+        src = r.get("achieved_source", "")
+        line["roofline"]["source"] = src.split(" (")[0][:160]
+    cb = out.get("cpu_baseline")
+    if isinstance(cb, dict):
+        c = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample", "gn_iters_per_s", "cpu") if k in cb}
+        pv = cb.get("poses_vs_gpu") or {}
+        c["poses_vs_gpu"] = {k: pv[k] for k in ("max_rot_diff_rad", "max_t_diff_m", "within_1e-4") if k in pv}
+        c["pytorch_cpu_fp64"] = {k: v.get("value") for k, v in (cb.get("pytorch_cpu_fp64") or {}).items()}
+        line["cpu_baseline"] = c
+    legs = {}
+    for k, v in out.items():
+        if k in _HEAD_KEYS or not isinstance(v, dict) or k in ("kernel_timing",):
+            continue
+        legs[k] = _leg_summary_compact(v)
+        for k2, v2 in v.items():  # one level of nested legs (full_pack, robotcar_1664, median_query_n295, ...)
+            if isinstance(v2, dict) and any(m in v2 for m in _MS_KEYS + _RATE_KEYS):
+                legs[f"{k}.{k2}"] = _leg_summary_compact(v2)
+    line["legs"] = legs
+    line["detail"] = detail_ref
+    text = json.dumps(line)
+    if len(text) > LINE_MAX_BYTES:  # never lose the headline to a long line: drop leg summaries last-first
+        for k in list(legs)[::-1]:
+            del legs[k]
+            line["legs_dropped"] = line.get("legs_dropped", 0) + 1
+            if len(json.dumps(line)) <= LINE_MAX_BYTES:
+                break
+    return line
 
 
 def free_port():
@@ -332,7 +423,8 @@ def main():
             out["rehearsal"] = (f"{world} ranks on {n_gpus} device(s): a rehearsal of the distributed path "
                                 f"(barrier + max-over-ranks timing), not a multi-GPU scaling figure")
         out.update(extras)
-        print(json.dumps(out), flush=True)
+        ref = write_detail(out, args.detail)
+        print(json.dumps(compact_line(out, ref)), flush=True)
     if dist:
         tdist.barrier()
         tdist.destroy_process_group()
