@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -76,9 +77,18 @@ int validate(const fmpnp_problem *probs, int n, const fmpnp_options *opt) {
 int device_cus(int *ncu) {
     // FMPNP_PLAN_CUS: plan for that many CUs without a device (host-side planner tests, the
     // sanitizer run of tools/sanitize.sh); the occupancy query then falls back to one block per CU
+    // (a test knob: on a host with a device it is ignored, with a note, so a stray value never
+    // changes a real launch's plan -- workgroups per problem, helpers -- or breaks the planner's
+    // all-resident assumption)
     if (const char *fc = getenv("FMPNP_PLAN_CUS")) {
-        *ncu = std::max(1, atoi(fc));
-        return 0;
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+            (void)hipGetLastError();
+            *ncu = std::max(1, atoi(fc));
+            return 0;
+        }
+        static std::once_flag note;
+        std::call_once(note, [] { fprintf(stderr, "fmpnp: FMPNP_PLAN_CUS ignored (a device is present)\n"); });
     }
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -155,7 +165,11 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
         // B=1 0.305 vs 0.313).  Larger problems keep spreading (cfg5, 2048 points at
         // C=512: G=4 0.64 ms vs G=32 0.58 ms at B=1)
         // (not bilinear: its memo builds are VALU work that more CUs share)
-        if (!streaming && !bil_memo && opt->layout == FMPNP_LAYOUT_FGRAD && P.nc_max <= 8) G = 1;
+        // (compute_cost is ONE evaluation in which every point gathers: bandwidth, not a latency
+        // chain, so it keeps the spread -- RobotCar C = 1664, 295 points: one workgroup 184 us)
+        if (!streaming && !bil_memo && opt->layout == FMPNP_LAYOUT_FGRAD && P.nc_max <= 8 &&
+            opt->mode == FMPNP_MODE_FORWARD)
+            G = 1;
         G = std::max(1, std::min(G, P.nc_max));
     }
     G = std::min(G, MAX_G);
@@ -220,7 +234,7 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
         // handed over, FMPNP_SS=2: prefetch only) take one spare CU per problem first.  Measured
         // slower than the speculation alone at every cap, so off by default.
         const char *es = getenv("FMPNP_SS");
-        const int ss = es ? std::max(0, std::min(2, atoi(es))) : 0;
+        const int ss = (FMPNP_SS && es) ? std::max(0, std::min(2, atoi(es))) : 0;
         if (ss && opt->helpers >= 0 && P.spec && G == 1 && P.wps == WPS_LATENCY && P.teams == n && spare >= 1) {
             P.ss = ss;
             --spare;
@@ -271,7 +285,7 @@ int fmpnp_abi_version(void) { return FMPNP_ABI_VERSION; }
 const char *fmpnp_build_info(void) {
     return "fmpnp gfx950: lm_kernel(NT=512 wave-owned blocks, CH=64, NV=32, fp64 accumulation, bilinear cell memo), "
            "pack_kernel(Sobel+HWC3), gather_ref_kernel; speculative_gathers=" FMPNP_STR(FMPNP_SPEC)
-           "; source_digest=" FMPNP_SOURCE_DIGEST;
+           "; steady_helpers=" FMPNP_STR(FMPNP_SS) "; source_digest=" FMPNP_SOURCE_DIGEST;
 }
 
 int fmpnp_device_check(int device) {

@@ -16,6 +16,13 @@
 #define FMPNP_SPEC 1
 #endif
 
+// Steady-state gather helpers (VAR_GM_SS / VAR_NEAREST_SS, opt-in FMPNP_SS=1|2 at run time): measured
+// slower than the speculation at every cap, so they are compiled only into a
+// -DFMPNP_SS=1 build (make EXTRA=-DFMPNP_SS=1) for repeating that measurement.
+#ifndef FMPNP_SS
+#define FMPNP_SS 0
+#endif
+
 namespace fmpnp {
 
 constexpr int NT = 512;         // threads per workgroup of the LM kernel (8 waves)

@@ -1,0 +1,226 @@
+// fmpnp_query.hip -- fmpnp_feature_pnp: one query of the reference adapter in ONE host call.
+//
+// feature_pnp (s2dhm/pose_prediction/optimize_feature_pnp.py:50-71) prepares a query on the
+// host -- fref gather, fp64 cast, Sobel -- and then runs forward or multilevel_optimization
+// (featurePnP/model.py:178-213, 245-494).  Here the whole call is one stream of device work
+// with a single host wait at the end:
+//
+//   H2D   reference inliers, 3D points and the launch descriptors, one copy from a pinned
+//         staging buffer the library owns (no pageable copies, no allocation per call);
+//   pack  the query map (fused Sobel + channels-last, or the f-only copy) into a cached buffer;
+//   fref  gather of the reference descriptors (out-of-map inliers set a device flag -- the
+//         reference's IndexError -- read with the results, no wait here);
+//   LM    forward over the whole map, or compute_cost + one forward per channel level, each
+//         level's initial pose copied from the previous level's result on the device;
+//   D2H   results (+ trace) and the flag, one copy, one stream synchronisation.
+//
+// The kernels are the ones the separate entry points launch, with the same descriptors, so the
+// results equal pack + gather + refine called one by one, bit for bit.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+
+#include "fmpnp.h"
+#include "fmpnp_internal.h"
+
+using namespace fmpnp;
+
+namespace {
+
+inline size_t al(size_t x) { return (x + 255) / 256 * 256; }
+
+// Per-process buffers of the one-query path: device memory on the device of the last call and a
+// pinned host staging buffer, both grown on demand and reused (one call at a time: the mutex is
+// held until the call's stream has drained, so no copy of an earlier call is still in flight).
+struct QueryCache {
+    std::mutex mu;
+    int device = -1;
+    unsigned char *dev = nullptr;
+    size_t dev_bytes = 0;
+    unsigned char *host = nullptr;  // pinned
+    size_t host_bytes = 0;
+};
+QueryCache g_q;
+
+int grow(QueryCache &c, int device, size_t dbytes, size_t hbytes) {
+    if (c.dev && (c.dev_bytes < dbytes || c.device != device)) {
+        int cur = device;
+        (void)hipSetDevice(c.device);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(c.dev);
+        (void)hipSetDevice(cur);
+        c.dev = nullptr;
+        c.dev_bytes = 0;
+    }
+    if (!c.dev) {
+        const size_t b = std::max(dbytes, (size_t)64 << 20);
+        if (hipMalloc((void **)&c.dev, b) != hipSuccess) {
+            c.dev = nullptr;
+            return FMPNP_ENOMEM;
+        }
+        c.dev_bytes = b;
+        c.device = device;
+    }
+    if (c.host_bytes < hbytes) {
+        if (c.host) (void)hipHostFree(c.host);
+        c.host = nullptr;
+        const size_t b = std::max(hbytes, (size_t)1 << 20);
+        if (hipHostMalloc((void **)&c.host, b, hipHostMallocDefault) != hipSuccess) {
+            c.host = nullptr;
+            c.host_bytes = 0;
+            return FMPNP_ENOMEM;
+        }
+        c.host_bytes = b;
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, int H, int W, const void *ref_chw,
+                                 int dtype_ref, int C_ref, int H_ref, int W_ref, const double *ref_inliers,
+                                 const double *pts3d, int N, const double K[9], const double R0[9], const double t0[3],
+                                 int img0, int img1, const fmpnp_level *levels, int n_levels,
+                                 const fmpnp_options *opt, fmpnp_result *results, fmpnp_trace_entry *trace,
+                                 int trace_stride, void *hip_stream) {
+    if (!query_chw || !ref_chw || !opt || !results || !K || !R0 || !t0 || N < 0 || C <= 0 || H <= 0 || W <= 0 ||
+        C_ref != C || H_ref <= 0 || W_ref <= 0 || img0 <= 0 || img1 <= 0 || n_levels < 0 || (n_levels > 0 && !levels))
+        return FMPNP_EINVAL;
+    if (N > 0 && (!ref_inliers || !pts3d)) return FMPNP_EINVAL;
+    if ((dtype_query != FMPNP_F32 && dtype_query != FMPNP_F64) || (dtype_ref != FMPNP_F32 && dtype_ref != FMPNP_F64))
+        return FMPNP_EINVAL;
+    if (opt->mode != FMPNP_MODE_FORWARD || (trace && trace_stride < 1)) return FMPNP_EINVAL;
+    for (int l = 0; l < n_levels; ++l)
+        if (levels[l].c_begin < 0 || levels[l].c_end <= levels[l].c_begin || levels[l].c_end > C) return FMPNP_EINVAL;
+    const bool lay_f = opt->layout == FMPNP_LAYOUT_F;
+    const int es = opt->dtype == FMPNP_F64 ? 8 : 4;
+    const int cs = (C + 3) / 4 * 4;
+    const int planes = lay_f ? 1 : 3;
+    const int n_fwd = n_levels > 0 ? n_levels : 1;
+    const int n_res = n_levels > 0 ? n_levels + 1 : 1;  // [compute_cost,] forward per level
+    const int stride = trace ? trace_stride : 0;
+
+    // host-side descriptors: [0] compute_cost over the whole map (levels only), then the forwards
+    fmpnp_problem hd[1 + 64];
+    if (n_res > 65) return FMPNP_EINVAL;
+    fmpnp_options oc = *opt;
+    oc.mode = FMPNP_MODE_COMPUTE_COST;  // model.py:216-243: squared, the whole channel range
+    oc.loss = FMPNP_SQUARED;
+    for (int r = 0; r < n_res; ++r) {
+        fmpnp_problem &p = hd[r];
+        memset(&p, 0, sizeof(p));
+        p.Hf = H;
+        p.Wf = W;
+        p.cstride = cs;
+        p.ld_ref = cs;
+        p.N = N;
+        p.im_width = img0;
+        p.im_height = img1;
+        memcpy(p.K, K, sizeof(p.K));
+        memcpy(p.R0, R0, sizeof(p.R0));
+        memcpy(p.t0, t0, sizeof(p.t0));
+        const int l = n_levels > 0 ? r - 1 : 0;
+        p.c_begin = (n_levels > 0 && r > 0) ? levels[l].c_begin : 0;
+        p.c_end = (n_levels > 0 && r > 0) ? levels[l].c_end : C;
+        // (pointers are set below, once the device buffer is placed; the plans need only sizes)
+        p.feat = p.fref = (const void *)(uintptr_t)256;
+        p.pts3d = (const double *)(uintptr_t)256;
+    }
+    // the LM workspace of the largest plan (the launches run one after another on the stream)
+    size_t ws = 0;
+    for (int r = 0; r < n_res; ++r) {
+        const size_t w = fmpnp_workspace_size(&hd[r], 1, (n_levels > 0 && r == 0) ? &oc : opt);
+        if (w == 0) return FMPNP_EINVAL;  // (fmpnp_workspace_size: invalid problem / options)
+        ws = std::max(ws, w);
+    }
+    // device carve: [inl | pts | descs] (the one upload), [results | err | trace] (the one
+    // download), the packed map, fref, the LM workspace
+    const size_t b_inl = al((size_t)N * 16), b_pts = al((size_t)N * 24), b_desc = al(sizeof(fmpnp_problem) * n_res);
+    const size_t b_res = al(sizeof(fmpnp_result) * n_res), b_err = 256;
+    const size_t b_tr = trace ? al(sizeof(fmpnp_trace_entry) * (size_t)n_fwd * stride) : 0;
+    const size_t b_feat = al((size_t)H * W * planes * cs * es), b_fref = al((size_t)std::max(N, 1) * cs * es);
+    const size_t up = b_inl + b_pts + b_desc, down = b_res + b_err + b_tr;
+    const size_t need = up + down + b_feat + b_fref + al(ws);
+
+    hipStream_t s = (hipStream_t)hip_stream;
+    std::lock_guard<std::mutex> lock(g_q.mu);
+    int device = 0;
+    hipError_t e = hipGetDevice(&device);
+    if (e != hipSuccess) return (int)e;
+    int rc = grow(g_q, device, need, up + down);
+    if (rc) return rc;
+    unsigned char *d = g_q.dev, *h = g_q.host;
+    double *d_inl = (double *)d, *d_pts = (double *)(d + b_inl);
+    fmpnp_problem *d_desc = (fmpnp_problem *)(d + b_inl + b_pts);
+    fmpnp_result *d_res = (fmpnp_result *)(d + up);
+    int *d_err = (int *)(d + up + b_res);
+    fmpnp_trace_entry *d_tr = trace ? (fmpnp_trace_entry *)(d + up + b_res + b_err) : nullptr;
+    unsigned char *d_feat = d + up + down, *d_fref = d_feat + b_feat, *d_ws = d_fref + b_fref;
+    for (int r = 0; r < n_res; ++r) {
+        hd[r].feat = d_feat;
+        hd[r].fref = d_fref;
+        hd[r].pts3d = d_pts;
+    }
+    // the one upload
+    if (N > 0) {
+        memcpy(h, ref_inliers, (size_t)N * 16);
+        memcpy(h + b_inl, pts3d, (size_t)N * 24);
+    }
+    memcpy(h + b_inl + b_pts, hd, sizeof(fmpnp_problem) * n_res);
+    e = hipMemcpyAsync(d, h, up, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return (int)e;
+    e = hipMemsetAsync(d_err, 0, sizeof(int), s);
+    if (e != hipSuccess) return (int)e;
+    if (trace) {
+        e = hipMemsetAsync(d_tr, 0, b_tr, s);
+        if (e != hipSuccess) return (int)e;
+    }
+    // pack (optimize_feature_pnp.py:57,61): the Sobel pack writes channels < C, so a padded
+    // stride is zeroed first; the f-only copy fills the padding itself
+    if (!lay_f && cs != C) {
+        e = hipMemsetAsync(d_feat, 0, b_feat, s);
+        if (e != hipSuccess) return (int)e;
+    }
+    e = launch_pack(query_chw, nullptr, nullptr, dtype_query, C, H, W, d_feat, opt->dtype, cs, opt->sobel_flags & 1,
+                    (opt->sobel_flags >> 1) & 1, s, planes);
+    if (e != hipSuccess) return (int)e;
+    // fref (optimize_feature_pnp.py:51-56): the reference map's first C channels
+    if (N > 0) {
+        if (cs != C) {
+            e = hipMemsetAsync(d_fref, 0, b_fref, s);
+            if (e != hipSuccess) return (int)e;
+        }
+        e = launch_gather_ref(ref_chw, dtype_ref, C_ref, H_ref, W_ref, d_inl, N, img0, img1, d_fref, opt->dtype, cs,
+                              d_err, s);
+        if (e != hipSuccess) return (int)e;
+    }
+    // the LM launches
+    for (int r = 0; r < n_res; ++r) {
+        const bool cost = n_levels > 0 && r == 0;
+        if (n_levels > 0 && r >= 2) {
+            // level r - 1 starts from level r - 2's result: R[9], t[3] -> R0[9], t0[3] (contiguous)
+            static_assert(offsetof(fmpnp_problem, t0) == offsetof(fmpnp_problem, R0) + 72, "R0, t0 contiguous");
+            static_assert(offsetof(fmpnp_result, t) == offsetof(fmpnp_result, R) + 72, "R, t contiguous");
+            e = hipMemcpyAsync((unsigned char *)(d_desc + r) + offsetof(fmpnp_problem, R0),
+                               (const unsigned char *)(d_res + r - 1) + offsetof(fmpnp_result, R), 96,
+                               hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) return (int)e;
+        }
+        fmpnp_trace_entry *tr = (trace && !cost) ? d_tr + (size_t)(n_levels > 0 ? r - 1 : 0) * stride : nullptr;
+        rc = fmpnp_refine_batch_async(d_desc + r, &hd[r], 1, N, cost ? &oc : opt, d_res + r, tr, stride, d_ws, ws,
+                                      hip_stream);
+        if (rc) return rc;
+    }
+    // the one download
+    e = hipMemcpyAsync(h, d_res, down, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return (int)e;
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return (int)e;
+    memcpy(results, h, sizeof(fmpnp_result) * n_res);
+    if (trace) memcpy(trace, h + b_res + b_err, sizeof(fmpnp_trace_entry) * (size_t)n_fwd * stride);
+    const int err = *(const int *)(h + b_res);
+    return err ? FMPNP_ERANGE : 0;
+}

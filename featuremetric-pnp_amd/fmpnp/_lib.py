@@ -22,13 +22,14 @@ MODE_FORWARD, MODE_COMPUTE_COST = 0, 1
 STATUS_OK, STATUS_NO_SUPPORT, STATUS_NAN, STATUS_NO_SUPPORT_TRIAL, STATUS_SYNC_TIMEOUT = 0, 1, 2, 4, 8
 STATUS_HELPER_WAIT = 16  # informational: a first-evaluation helper did not publish in time (results unaffected)
 STATUS_WINDOW = 32  # a point left its packed window (fmpnp_pack_features_f_window_batch): result invalid, re-run
-ABI_VERSION = 3
+ABI_VERSION = 4
 # LM kernel builds and variants (fmpnp_launch_info)
 BUILD_WIDE, BUILD_LATENCY, BUILD_THROUGHPUT = 1, 2, 4
 BUILD_NAMES = {BUILD_WIDE: "wide", BUILD_LATENCY: "latency", BUILD_THROUGHPUT: "throughput"}
 VARIANT_NAMES = ["NEAREST", "GM", "BILINEAR", "F_NEAREST", "F_GM", "BIL_DIRECT", "GM_SPEC", "NEAREST_SPEC",
                  "GM_SPEC_H", "NEAREST_SPEC_H", "GM_H", "NEAREST_H", "GM_SS", "NEAREST_SS"]
-ERRORS = {-1: "EINVAL", -2: "EALIGN", -3: "ENOMEM", -4: "ETOOBIG", -5: "ENODEV"}
+ERRORS = {-1: "EINVAL", -2: "EALIGN", -3: "ENOMEM", -4: "ETOOBIG", -5: "ENODEV", -6: "ERANGE"}
+ERANGE = -6  # fmpnp_feature_pnp: a reference inlier outside the reference map (IndexError)
 
 
 class Options(ctypes.Structure):
@@ -46,6 +47,10 @@ class Problem(ctypes.Structure):
                 ("im_width", ctypes.c_int), ("im_height", ctypes.c_int),
                 ("K", ctypes.c_double * 9), ("R0", ctypes.c_double * 9), ("t0", ctypes.c_double * 3),
                 ("window", ctypes.c_void_p)]
+
+
+class Level(ctypes.Structure):
+    _fields_ = [("c_begin", ctypes.c_int), ("c_end", ctypes.c_int)]
 
 
 class Result(ctypes.Structure):
@@ -73,7 +78,7 @@ EXPORTS = ["fmpnp_abi_version", "fmpnp_build_info", "fmpnp_device_check", "fmpnp
            "fmpnp_gather_reference", "fmpnp_gather_reference_async", "fmpnp_pack_features_batch", "fmpnp_pack_features_f",
            "fmpnp_gather_reference_batch", "fmpnp_workspace_size", "fmpnp_refine_batch_async", "fmpnp_refine_batch",
            "fmpnp_last_launch", "fmpnp_debug_stamps", "fmpnp_plan", "fmpnp_last_launch_info",
-           "fmpnp_pack_features_f_window_batch"]
+           "fmpnp_pack_features_f_window_batch", "fmpnp_feature_pnp"]
 
 _LIB = None
 
@@ -126,6 +131,10 @@ def load():
     L.fmpnp_plan.restype = i
     L.fmpnp_last_launch_info.argtypes = [ctypes.POINTER(LaunchInfo)]
     L.fmpnp_last_launch_info.restype = i
+    dp = ctypes.POINTER(ctypes.c_double)
+    L.fmpnp_feature_pnp.argtypes = [vp, i, i, i, i, vp, i, i, i, i, vp, vp, i, dp, dp, dp, i, i,
+                                    ctypes.POINTER(Level), i, ctypes.POINTER(Options), vp, vp, i, vp]
+    L.fmpnp_feature_pnp.restype = i
     if L.fmpnp_abi_version() != ABI_VERSION:
         raise FmpnpError("libfmpnp ABI mismatch")
     _LIB = L

@@ -17,9 +17,11 @@ def kernel_name(info):
 SOURCE_FILES = ("featuremetric-pnp_amd/Makefile", "featuremetric-pnp_amd/csrc", "include/fmpnp.h")
 
 
-def source_digest(root=None):
-    """sha256 (16 hex digits) over the library's source files, path and content: identifies the
-    build a profile was taken with on a box that has no git history (gpurun ships the tree)."""
+def source_digest(root=None, flags=""):
+    """sha256 (16 hex digits) over the library's source files, path and content, and the compile
+    flags (the Makefile passes its effective FLAGS, so a build with other -D options or another
+    ARCH gets another digest): identifies the build a profile was taken with on a box that has no
+    git history (gpurun ships the tree)."""
     import hashlib
     root = root or os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     files = []
@@ -36,4 +38,20 @@ def source_digest(root=None):
         with open(os.path.join(root, rel), "rb") as f:
             h.update(f.read())
         h.update(b"\0")
+    if flags:
+        h.update(b"flags\0" + " ".join(flags.split()).encode())
     return h.hexdigest()[:16]
+
+
+def library_file_digest(path=None):
+    """The digest compiled into a built libfmpnp.so (its fmpnp_build_info string), read from the
+    file without loading it: what the profiling tools record, so a profile names the build it
+    was taken with, flags included."""
+    import re
+    path = path or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libfmpnp.so")
+    try:
+        with open(path, "rb") as f:
+            m = re.search(rb"source_digest=([0-9a-z]{7,16})", f.read())
+    except OSError:
+        return "unknown"
+    return m.group(1).decode() if m else "unknown"

@@ -100,6 +100,12 @@ class sparseFeaturePnP(nn.Module):
         opts = self._options(feats.dtype_code)
         want_trace = bool(track) or bool(self.verbose)
         (res,), traces = _rf.refine([prob], opts, trace=want_trace)
+        return self._apply_result(res, traces[0] if traces is not None else None, pts_np, K, im_width, im_height,
+                                  track, prob)
+
+    def _apply_result(self, res, tr, pts_np, K, im_width, im_height, track, prob=None):
+        """One forward's result (and trace) -> the reference's attributes, track_ entries and
+        verbose lines (model.py:347-361, 464-468, 477-494); returns (R, t) as fp64 CPU tensors."""
         self.last_result_ = res
         # (FMPNP_STATUS_HELPER_WAIT is informational -- a first-evaluation helper workgroup was not
         # resident in time and the main workgroup gathered itself, results unchanged -- so it is not
@@ -110,8 +116,7 @@ class sparseFeaturePnP(nn.Module):
             self.best_num_inliers_ = int(res["best_num_inliers"])
             if self.initial_cost_ is None:
                 self.initial_cost_ = torch.tensor(res["initial_cost"], dtype=torch.float64)
-        if traces is not None:
-            tr = traces[0]
+        if tr is not None:
             Kn = _to_np(K, (3, 3))
             for k in range(len(tr["cost"])):
                 if self.verbose:

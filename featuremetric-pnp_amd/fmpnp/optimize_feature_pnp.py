@@ -27,14 +27,15 @@ def feature_pnp_multi(query_hypercolumns, reference_hypercolumns, prediction, K,
     """optimize_feature_pnp.py:20-47: refine on the current inliers, re-select the inliers
     with find_inliers at the new pose, three times.  The initial inliers are
     prediction.inlier_mask, or find_inliers at the initial pose when it is None.  The query
-    map is packed once (f-only layout for fp32 texels); every round reuses it and the
+    map is packed once (f, gx, gy planes); every round reuses it and the
     device fref.  Returns (R, t, model) like feature_pnp."""
     model = _new_model(model)
     q = query_hypercolumns[0] if query_hypercolumns.dim() == 4 else query_hypercolumns
     dev = q.device if q.is_cuda else torch.device("cuda", torch.cuda.current_device())
     storage = storage or model.storage or (torch.float64 if q.dtype == torch.float64 else torch.float32)
-    layout = "f" if storage == torch.float32 and getattr(model, "sampling", "nearest") == "nearest" else "fgrad"
-    feats = _rf.pack_features(q, storage=storage, device=dev, layout=layout)               # :28,31
+    # (three LM launches and four point-cost launches on one map: the packed f/gx/gy planes, as
+    # feature_pnp -- the LM reads 16C bytes per gathered texel from them against 40C from "f")
+    feats = _rf.pack_features(q, storage=storage, device=dev, layout="fgrad")              # :28,31
     fref = _rf.gather_reference(reference_hypercolumns, prediction.reference_inliers, image_shape,
                                 cstride=feats.cstride, storage=storage, device=dev)          # :21-26
     pts3D = np.asarray(prediction.points_3d, dtype=np.float64).reshape(-1, 3)               # :22
@@ -59,16 +60,21 @@ def feature_pnp(query_hypercolumns, reference_hypercolumns, prediction, K, image
                 feature_pyramid=None, model=None, storage=None, layout=None):
     """optimize_feature_pnp.py:50-71.  Returns (R, t, model) with R, t fp64 CPU tensors.
 
-    layout: None picks the f-only layout (FMPNP_LAYOUT_F: the LM kernel forms the fp64 Sobel
-    gradients, a third of the pack's bytes) for fp32 texels with nearest sampling and no
-    pyramid, else the packed f/gx/gy planes ("fgrad")."""
+    layout: None (default) packs the f/gx/gy planes ("fgrad": the fused Sobel + channels-last
+    pack); "f" packs f only (FMPNP_LAYOUT_F: a third of the pack's bytes, the LM kernel forms
+    the fp64 Sobel gradients of every texel it gathers).  One query per call is LM-bound, and
+    the LM reads 16C bytes per gathered texel from "fgrad" against 40C from "f": cfg2, one
+    call, pack + LM 66 + 259 us against 33 + 559 us (rocprofv3, profiles/r05_facade_*)."""
     model = _new_model(model)
     q = query_hypercolumns[0] if query_hypercolumns.dim() == 4 else query_hypercolumns
     dev = q.device if q.is_cuda else torch.device("cuda", torch.cuda.current_device())
     storage = storage or model.storage or (torch.float64 if q.dtype == torch.float64 else torch.float32)
     if layout is None:
-        layout = ("f" if storage == torch.float32 and feature_pyramid is None
-                  and getattr(model, "sampling", "nearest") == "nearest" else "fgrad")
+        layout = "fgrad"
+    levels = _channel_levels(feature_pyramid, q.shape[0])
+    if _one_call_ok(model, q, reference_hypercolumns, feature_pyramid, levels, track, storage, layout):
+        return _feature_pnp_one_call(model, q, reference_hypercolumns, prediction, K, image_shape, track, levels,
+                                     storage, layout)
     feats = _rf.pack_features(q, storage=storage, device=dev, layout=layout)               # :57, :61
     fref = _rf.gather_reference(reference_hypercolumns, prediction.reference_inliers, image_shape,
                                 cstride=feats.cstride, storage=storage, device=dev)          # :51-56
@@ -81,6 +87,94 @@ def feature_pnp(query_hypercolumns, reference_hypercolumns, prediction, K, image
     else:
         R, t = model._multilevel_packed(feature_pyramid, feats, q, pts3D, fref, Kt, image_shape[0], image_shape[1],
                                         R, t, track)
+    return R, t, model
+
+
+def _channel_levels(feature_pyramid, C):
+    """multilevel_optimization's levels (model.py:193-194) as channel ranges [start, min(end, C))
+    when every level is a plain channel slice (no resize, no blur); None otherwise."""
+    if feature_pyramid is None:
+        return None
+    out = []
+    for start, end, target_size, kernel_size in feature_pyramid:
+        if target_size is not None or kernel_size is not None:
+            return None
+        out.append((int(start), min(int(end), C)))  # python slicing clamps (model.py:194)
+    return out
+
+
+def _one_call_ok(model, q, r, feature_pyramid, levels, track, storage, layout):
+    """fmpnp_feature_pnp runs the whole call (pack, gather, compute_cost, every level) with one
+    host wait when both maps are device tensors of the same device and channel count and the
+    pyramid is channel slices only; track_ with the ratio test needs the packed map for its
+    threshold masks (fmpnp_point_costs), so that case takes the step-by-step path."""
+    r = r[0] if r.dim() == 4 else r
+    ok = (q.is_cuda and r.is_cuda and q.device == r.device and q.dim() == 3 and r.dim() == 3
+          and q.dtype in (torch.float32, torch.float64) and r.dtype in (torch.float32, torch.float64)
+          and r.shape[0] == q.shape[0] and storage in (torch.float32, torch.float64)
+          and not (track and model.use_ratio_test_) and (layout == "fgrad" or storage == torch.float32))
+    if feature_pyramid is not None:
+        ok = ok and levels is not None and len(levels) > 0 and all(0 <= a < b for a, b in levels)
+    return ok
+
+
+def _feature_pnp_one_call(model, q, r, prediction, K, image_shape, track, levels, storage, layout):
+    """feature_pnp through fmpnp_feature_pnp: one host call, one host wait (optimize_feature_pnp.py:50-71)."""
+    import ctypes
+    from . import _lib
+    r = r[0] if r.dim() == 4 else r
+    q, r = q.contiguous(), r.contiguous()
+    dev = q.device
+    C, H, W = q.shape
+    opts = model._options(_rf._dtype_code(storage))
+    opts.layout = _lib.LAYOUT_F if layout == "f" else _lib.LAYOUT_FGRAD
+    opts.sobel_flags = 0
+    inl = np.ascontiguousarray(np.asarray(prediction.reference_inliers, dtype=np.float64).reshape(-1, 2))  # :53
+    pts = np.ascontiguousarray(np.asarray(prediction.points_3d, dtype=np.float64).reshape(-1, 3))          # :52
+    if inl.shape[0] != pts.shape[0]:
+        raise ValueError("reference_inliers and points_3d must have one row per match")
+    T = np.asarray(prediction.matrix, dtype=np.float64)
+    R0, t0 = np.ascontiguousarray(T[:3, :3]), np.ascontiguousarray(T[:3, 3])                            # :59-60
+    Kn = np.ascontiguousarray((K.detach().cpu().numpy() if isinstance(K, torch.Tensor) else np.asarray(K))
+                              .astype(np.float64).reshape(3, 3))
+    n_lv = len(levels) if levels else 0
+    lv = (_lib.Level * max(n_lv, 1))(*[_lib.Level(a, b) for a, b in (levels or [])])
+    res = np.zeros(n_lv + 1 if n_lv else 1, dtype=_rf.RESULT_DTYPE)
+    want_trace = bool(track) or bool(model.verbose)
+    stride = model.iterations + 1
+    tr = (_lib.TraceEntry * (max(n_lv, 1) * stride))() if want_trace else None
+    dp = ctypes.POINTER(ctypes.c_double)
+    vp = ctypes.c_void_p
+    with torch.cuda.device(dev):
+        rc = _lib.load().fmpnp_feature_pnp(
+            vp(q.data_ptr()), _rf._dtype_code(q.dtype), C, H, W, vp(r.data_ptr()), _rf._dtype_code(r.dtype),
+            r.shape[0], r.shape[1], r.shape[2], vp(inl.ctypes.data), vp(pts.ctypes.data), pts.shape[0],
+            Kn.ctypes.data_as(dp), R0.ctypes.data_as(dp), t0.ctypes.data_as(dp), int(image_shape[0]),
+            int(image_shape[1]), lv if n_lv else None, n_lv, ctypes.byref(opts), vp(res.ctypes.data), tr,
+            stride if want_trace else 0, _lib.stream_ptr(dev))
+    if rc == _lib.ERANGE:
+        raise IndexError("a reference inlier maps outside the reference hypercolumn "
+                         "(optimize_feature_pnp.py:56 raises IndexError)")
+    _lib.check(rc, "fmpnp_feature_pnp")
+    out = _rf.results_from_array(res)
+    if any(x["status"] & _lib.STATUS_SYNC_TIMEOUT for x in out):
+        raise _lib.FmpnpError("cross-workgroup exchange timed out (device oversubscribed?)")
+    W_img, H_img = image_shape[0], image_shape[1]
+
+    def trace_of(i, n_evals):
+        return _rf._trace_dict(tr[i * stride:(i + 1) * stride], n_evals) if want_trace else None
+    if not n_lv:                                                                            # :64-65
+        R, t = model._apply_result(out[0], trace_of(0, out[0]["n_evals"]), pts, Kn, W_img, H_img, track)
+        return R, t, model
+    # multilevel_optimization (model.py:178-213): initial_cost_ from compute_cost; no support -> the
+    # initial pose, unrefined (:183-187); else each level's forward from the previous level's pose
+    cost = out[0]
+    if cost["status"] & _lib.STATUS_NO_SUPPORT:
+        model.initial_cost_ = None
+        return torch.from_numpy(R0.copy()), torch.from_numpy(t0.copy()), model
+    model.initial_cost_ = torch.tensor(cost["initial_cost"], dtype=torch.float64)
+    for li in range(n_lv):
+        R, t = model._apply_result(out[1 + li], trace_of(li, out[1 + li]["n_evals"]), pts, Kn, W_img, H_img, track)
     return R, t, model
 
 

@@ -70,10 +70,15 @@ class _LevelChain:
         return [t for b in self.levels for t in (b.d_descs, b.d_res, b.d_ws)]
 
     def results(self):
+        """The last level's results; every level's status in `level_status`, and the bits that say
+        an earlier level went wrong ORed in: a timed-out exchange (its poses unrefined) and a NaN
+        step (model.py:411-413) -- both seed the next level with a pose that was not refined."""
         res = self.levels[-1].results()
-        for b in self.levels[:-1]:  # a timed-out exchange in any level left its poses unrefined
-            for r, e in zip(res, b.results()):
-                r["status"] |= e["status"] & _lib.STATUS_SYNC_TIMEOUT
+        earlier = [b.results() for b in self.levels[:-1]]
+        for q, r in enumerate(res):
+            r["level_status"] = [e[q]["status"] for e in earlier] + [r["status"]]
+            for e in earlier:
+                r["status"] |= e[q]["status"] & (_lib.STATUS_SYNC_TIMEOUT | _lib.STATUS_NAN)
         return res
 
 
@@ -116,6 +121,7 @@ class RefinePipeline:
         if self.window is not None and (self.layout != "f" or self.window < 2):
             raise ValueError("window needs the f-only layout and a radius >= 2")
         self.refills = 0  # queries re-run with the full pack after leaving their window
+        self.unwindowed_batches = 0  # batches packed in full: a problem too large for a windowed plan
         self.levels = [tuple(int(c) for c in lv) for lv in levels] if levels else None
         if self.levels and self.window is not None:
             raise ValueError("channel levels run on fully packed maps (window=None)")
@@ -223,6 +229,16 @@ class RefinePipeline:
             if self.window is not None:
                 desc["window"] = out_ptrs + (Hs * Ws * css * es + _ALIGN - 1) // _ALIGN * _ALIGN
             opts = self.batch_options(nq)
+            windowed = self.window is not None and self._window_fits(desc, opts)
+            if self.window is not None and not windowed:
+                # a packed window takes one workgroup per problem; a problem too large for one
+                # workgroup's LDS (fmpnp_api.hip make_plan: ETOOBIG) gets this batch fully packed
+                desc["window"] = 0
+                self.unwindowed_batches += 1
+                rc = L.fmpnp_pack_features_batch(
+                    nq, (vp * nq)(*[m.data_ptr() for m in qmaps]), (vp * nq)(*out_ptrs.tolist()), shape_arr,
+                    _rf._dtype_code(q_dt), _rf._dtype_code(storage), 0, 0, _lib.LAYOUT_F, s)
+                _lib.check(rc, "fmpnp_pack_features_batch")
             if self.levels:
                 chain = []
                 for cb, ce in self.levels:
@@ -234,7 +250,7 @@ class RefinePipeline:
                 batch = _LevelChain(chain)
             else:
                 batch = _rf.AsyncBatch.from_descriptors(desc, opts, dev, non_blocking=True)
-            if self.window is not None:  # the windowed pack reads the uploaded descriptors
+            if windowed:  # the windowed pack reads the uploaded descriptors
                 rc = L.fmpnp_pack_features_f_window_batch(
                     vp(batch.d_descs.data_ptr()), vp(batch.descs_np.ctypes.data), nq, (vp * nq)(*[m.data_ptr() for m in qmaps]),
                     _rf._dtype_code(q_dt), self.window, s)                                     # :57, :61
@@ -242,6 +258,14 @@ class RefinePipeline:
         # read on the prep stream (maps, converted copies) or the solve stream (the rest):
         # kept alive until the batch is collected
         return batch, [qmaps, rmaps, fbuf, dflat, desc], err
+
+    def _window_fits(self, desc, opts):
+        """Whether the batch's windowed launch plan exists (one workgroup per problem must hold
+        the largest problem in its LDS)."""
+        d = desc.copy()
+        d["window"] = 1 << 12  # (any non-null pointer: the plan reads sizes only)
+        return _lib.load().fmpnp_workspace_size(d.ctypes.data_as(ctypes.POINTER(_lib.Problem)), len(d),
+                                                ctypes.byref(opts)) != 0
 
     def _refill(self, res, keep):
         """Queries that left their packed window: pack their maps in full and refine them again

@@ -82,7 +82,7 @@ def problem_inputs(N=512, C=256, Hf=240, Wf=320, seed=0, device="cuda", init="ea
 QueryPrediction = namedtuple("QueryPrediction", "points_3d reference_inliers matrix")
 
 
-def pipeline_queries(n_batches, batch, N=512, C=256, Hf=240, Wf=320, device="cuda", seed0=0):
+def pipeline_queries(n_batches, batch, N=512, C=256, Hf=240, Wf=320, device="cuda", seed0=0, init="easy"):
     """Batches of feature_pnp-style queries (query_hc, reference_hc, prediction, K) for
     fmpnp.pipeline.RefinePipeline, and the image_shape (W, H) they use.  The reference
     hypercolumn is the query map; the reference inliers are placed so that the reference's
@@ -102,7 +102,7 @@ def pipeline_queries(n_batches, batch, N=512, C=256, Hf=240, Wf=320, device="cud
             cols = (p[:, 0].astype(np.int64) * Wf) // W
             inl = np.stack([(cols + 0.5) * W / Hf, (rows + 0.5) * H / Wf], 1)
             T = np.eye(4)
-            T[:3, :3], T[:3, 3] = rot_z(1.0), np.array([0.05, -0.03, 0.10])
+            T[:3, :3], T[:3, 3] = INITS[init]
             qs.append((fmap, fmap[None], QueryPrediction(X, inl, T), K))
         batches.append(qs)
     return batches, (W, H)

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define FMPNP_ABI_VERSION 3  /* 3: fmpnp_problem.window (windowed f-only packs) */
+#define FMPNP_ABI_VERSION 4  /* 3: fmpnp_problem.window (windowed f-only packs); 4: fmpnp_feature_pnp */
 
 /* robust losses, featurePnP/helpers/utils.py:15-78 */
 typedef enum {
@@ -92,6 +92,8 @@ typedef enum {
 #define FMPNP_ENOMEM -3
 #define FMPNP_ETOOBIG -4
 #define FMPNP_ENODEV -5
+#define FMPNP_ERANGE -6  /* fmpnp_feature_pnp: a reference inlier maps outside the reference map
+                            (the reference raises IndexError, optimize_feature_pnp.py:56) */
 
 typedef struct {
     int mode;               /* fmpnp_mode */
@@ -251,6 +253,34 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
  * hip_stream and waits for that stream. */
 int fmpnp_refine_batch(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt, fmpnp_result *results,
                        fmpnp_trace_entry *trace, int trace_stride, void *hip_stream);
+
+/* One channel level of multilevel_optimization's pyramid (featurePnP/model.py:193-210): the
+ * channel range [c_begin, c_end) of the query map (input_configs/default_robotcar.gin:75). */
+typedef struct {
+    int c_begin, c_end;
+} fmpnp_level;
+
+/* One query of feature_pnp (s2dhm/pose_prediction/optimize_feature_pnp.py:50-71) in one call,
+ * with one host wait: pack the query map (opt->layout; opt->sobel_flags are the Sobel's flags),
+ * gather the reference descriptors of the N reference inliers (x, y) with the adapter's
+ * truncation, then
+ *   n_levels == 0: forward over channels [0, C)                     (model.py:245-494)
+ *                  -> results[0];
+ *   n_levels >  0: multilevel_optimization over the channel levels  (model.py:178-213):
+ *                  compute_cost at (R0, t0) over [0, C) -> results[0] (status NO_SUPPORT: the
+ *                  reference returns (R0, t0) without refining -- the caller applies that), then
+ *                  forward per level, each from the previous level's result pose -> results[1 + l].
+ * query_chw [C][H][W] and ref_chw [C_ref][H_ref][W_ref] (C_ref == C) are DEVICE maps; ref_inliers
+ * [N][2], pts3d [N][3], K, R0, t0 (row-major) and results / trace ([max(n_levels, 1)][trace_stride]
+ * entries, or NULL) are HOST memory.  opt->mode must be FMPNP_MODE_FORWARD; opt->dtype is the
+ * packed storage.  Returns 0, FMPNP_ERANGE when an inlier maps outside the reference map (results
+ * are still written), another FMPNP_E* code or a hipError_t.  The library keeps the device buffers
+ * and a pinned staging buffer between calls (one call at a time per process). */
+int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, int H, int W, const void *ref_chw,
+                      int dtype_ref, int C_ref, int H_ref, int W_ref, const double *ref_inliers,
+                      const double *pts3d, int N, const double K[9], const double R0[9], const double t0[3],
+                      int img0, int img1, const fmpnp_level *levels, int n_levels, const fmpnp_options *opt,
+                      fmpnp_result *results, fmpnp_trace_entry *trace, int trace_stride, void *hip_stream);
 
 /* Debug: when device_buf != NULL, later LM launches write per-workgroup phase cycle
  * totals (s_memtime) to device_buf[grid][8 waves][12] (8 phases, then the first evaluation's

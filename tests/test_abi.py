@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     L = _lib.load()
     missing = [f for f in declared_functions() if not hasattr(L, f)]
     assert not missing, missing
-    assert L.fmpnp_abi_version() == _lib.ABI_VERSION == 3
+    assert L.fmpnp_abi_version() == _lib.ABI_VERSION == 4
     assert b"gfx950" in L.fmpnp_build_info()
 
 
@@ -43,7 +43,7 @@ def test_library_is_a_gfx950_code_object():
 
 
 STRUCTS = {"fmpnp_options": _lib.Options, "fmpnp_problem": _lib.Problem, "fmpnp_result": _lib.Result,
-           "fmpnp_trace_entry": _lib.TraceEntry, "fmpnp_launch_info": _lib.LaunchInfo}
+           "fmpnp_trace_entry": _lib.TraceEntry, "fmpnp_launch_info": _lib.LaunchInfo, "fmpnp_level": _lib.Level}
 
 
 @pytest.mark.parametrize("name", sorted(STRUCTS))
@@ -143,3 +143,34 @@ def test_window_pack_rejects_bad_arguments_without_a_device():
         setattr(q, field, bad)
         assert L.fmpnp_pack_features_f_window_batch(256, ctypes.byref(q), 1, chw, 0, 3, None) == -1, field
     assert L.fmpnp_pack_features_f_window_batch(256, ctypes.byref(p), 0, chw, 0, 3, None) == 0      # nothing to do
+
+
+def test_feature_pnp_call_rejects_bad_arguments_without_a_device():
+    """fmpnp_feature_pnp (one query of feature_pnp per call) validates its arguments before any
+    device call: missing maps or outputs, a reference map of another channel count, a bad level,
+    a compute_cost mode, an unknown dtype."""
+    import numpy as np
+    L = _lib.load()
+    vp = ctypes.c_void_p
+    dp = ctypes.POINTER(ctypes.c_double)
+    K = np.eye(3).reshape(-1)
+    inl, pts = np.zeros((4, 2)), np.ones((4, 3))
+    o = _lib.Options()
+    res = (_lib.Result * 4)()
+
+    def call(q=4096, C=8, Cr=8, lv=None, nlv=0, opt=o, res_=res, dq=0, N=4):
+        arr = (_lib.Level * max(nlv, 1))(*(lv or []))
+        return L.fmpnp_feature_pnp(vp(q) if q else None, dq, C, 16, 16, vp(4096), 0, Cr, 16, 16,
+                                   vp(inl.ctypes.data), vp(pts.ctypes.data), N, K.ctypes.data_as(dp),
+                                   K.ctypes.data_as(dp), K[:3].ctypes.data_as(dp), 64, 64,
+                                   arr if nlv else None, nlv, ctypes.byref(opt), res_, None, 0, None)
+    assert call(q=0) == -1                                   # no query map
+    assert call(Cr=9) == -1                                  # reference map of another channel count
+    assert call(dq=3) == -1                                  # unknown dtype
+    assert call(N=-1) == -1
+    assert call(lv=[_lib.Level(0, 9)], nlv=1) == -1          # level beyond the map's channels
+    assert call(lv=[_lib.Level(4, 4)], nlv=1) == -1          # empty level
+    assert call(res_=None) == -1
+    oc = _lib.Options.from_buffer_copy(o)
+    oc.mode = _lib.MODE_COMPUTE_COST
+    assert call(opt=oc) == -1                                # forward only (compute_cost runs inside)

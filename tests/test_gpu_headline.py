@@ -331,7 +331,9 @@ def test_steady_helpers_change_nothing(B, init, ratio, loss, monkeypatch):
     query predicts and gathers the next evaluation's texels on an idle CU; =2: they only prefetch)
     move work, never a result: poses, costs, the schedule and the per-evaluation support are
     bit-identical to the speculating variant, over repeated launches (the hand-off's tags are
-    launch-unique)."""
+    launch-unique).  Compiled only into a -DFMPNP_SS=1 build (measured slower)."""
+    if b"steady_helpers=1" not in _lib.load().fmpnp_build_info():
+        pytest.skip("steady-state helpers not compiled in (make EXTRA=-DFMPNP_SS=1)")
     probs = [packed_problem(synth.problem_inputs(512, 256, 240, 320, seed=q, device=DEV, init=init))
              for q in range(B)]
     code, var = (_lib.GEMAN_MCCLURE, "GM") if loss == "gm" else (_lib.CAUCHY, "NEAREST")

@@ -59,8 +59,13 @@ def test_headline_plan():
 
 def test_steady_helpers_opt_in(monkeypatch):
     """FMPNP_SS=1|2 plans the steady-state gather helpers (one per query on a spare CU); they stay
-    off without a spare CU per problem and with options.helpers < 0 (a shared device)."""
+    off without a spare CU per problem and with options.helpers < 0 (a shared device).  Only in a
+    -DFMPNP_SS=1 build; the default build never plans them."""
     monkeypatch.setenv("FMPNP_SS", "1")
+    if b"steady_helpers=1" not in _lib.load().fmpnp_build_info():
+        i = plan(128, rf.make_options(**GM))
+        assert (i["grid"], i["variant_name"]) == (128, "GM_SPEC")
+        return
     i = plan(128, rf.make_options(**GM))
     assert (i["grid"], i["variant_name"], i["helpers"]) == (256, "GM_SS", 0)
     i = plan(128, rf.make_options(**dict(GM, loss=_lib.CAUCHY)))

@@ -64,7 +64,7 @@ def main():
            "hbm_bytes_per_query": sum(v["hbm_bytes_per_query"] for v in fams.values()),
            "kernel_ns_per_query": sum(v["kernel_ns_per_query"] for v in fams.values()),
            "correction": "FETCH_SIZE x2 (gfx950 wide-read halving), KiB -> bytes",
-           "source_digest": build_id().source_digest(ROOT), "git_head": os.environ.get("GIT_HEAD") or None}
+           "source_digest": build_id().library_file_digest(os.environ.get("FMPNP_LIB_PATH")), "git_head": os.environ.get("GIT_HEAD") or None}
     with open(os.path.join(d, "summary.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))

@@ -49,7 +49,7 @@ def main():
     out = {"workload": f"RobotCar pyramid, B=32, C=1664 256x256, N={N}, GM, 50 iters per level "
                        "(tools/pyramid_run.py)", "N": N, "levels": levels,
            "correction": "FETCH_SIZE x2 (gfx950 wide-read halving), KiB -> bytes",
-           "source_digest": build_id().source_digest(ROOT), "git_head": os.environ.get("GIT_HEAD") or None}
+           "source_digest": build_id().library_file_digest(os.environ.get("FMPNP_LIB_PATH")), "git_head": os.environ.get("GIT_HEAD") or None}
     with open(os.path.join(d, "summary.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))

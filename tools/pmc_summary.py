@@ -75,7 +75,7 @@ def main():
         "correction": "FETCH_SIZE x2 (gfx950 wide-read halving), KiB -> bytes",
         # the build the counters were taken with: bench.py uses the bytes only for this digest and
         # this kernel specialisation (GIT_HEAD: set by the caller; the box has no git history)
-        "source_digest": build_id().source_digest(ROOT),
+        "source_digest": build_id().library_file_digest(os.environ.get("FMPNP_LIB_PATH")),
         "git_head": os.environ.get("GIT_HEAD") or None,
         "all_kernels": [{k: r[k] for k in ("Name", "Calls", "AverageNs", "Percentage") if k in r} for r in stats],
     }
