@@ -15,7 +15,11 @@ from golden_io import ADAPTER_CASES, load_npz
 pytestmark = pytest.mark.gpu
 
 import fmpnp  # noqa: E402
-from fmpnp import optimize_feature_pnp as ofp, synth  # noqa: E402
+import importlib  # noqa: E402
+
+from fmpnp import synth  # noqa: E402
+
+ofp = importlib.import_module("fmpnp.optimize_feature_pnp")  # (the package re-exports the function under the module name)
 
 DEV = "cuda:0"
 Pred = namedtuple("Prediction", "points_3d reference_inliers matrix quaternion reference_filename")

@@ -382,3 +382,19 @@ def test_ratio_guess_changes_nothing(B, init, ratio, monkeypatch):
     assert sum(r["texel_gathers"] >> 32 for r in base) == 8 * evals  # (forced: every block of every evaluation)
     print(f"B={B} {init} ratio {ratio}: re-formed {redo} of {8 * evals} blocks")
     assert redo < 4 * evals
+
+
+@pytest.mark.parametrize("B", [1, 128])
+def test_cfg0_toy_shape_against_oracle(B):
+    """configs[0]'s stated shape (featurePnP/toy_example: N=64 points, C=3, 120x160, squared loss,
+    20 GN iterations), batch 1 and 128 distinct maps in one launch, each against its own oracle
+    run (the toy-6 KAT covers the reference's own toy data, tests/test_gpu_parity.py)."""
+    inps = [synth.problem_inputs(64, 3, 120, 160, seed=300 + q, device=DEV) for q in range(B)]
+    hosts = [host_copy(i) for i in inps]
+    probs = [packed_problem(i) for i in inps]
+    del inps
+    res, trs = rf.refine(probs, rf.make_options(20, 0.01, _lib.SQUARED, dtype=_lib.F32), trace=True)
+    with ThreadPoolExecutor(8) as ex:
+        oracle = list(ex.map(lambda h: oracle_run(h, n_iters=20, loss="squared"), hosts))
+    for q in range(B):
+        check(res[q], trs[q], *oracle[q], f"toy query {q}")
