@@ -499,6 +499,12 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
         a.spec_w0 = ew ? std::max(0, atoi(ew)) : 3;  // round 3: wave 3 (no tail role) speculates too
     }
     {
+        // the ratio test's form per evaluation (measurement knob FMPNP_RATIO_GTHR; 0 = always the
+        // guessed limit)
+        const char *e = getenv("FMPNP_RATIO_GTHR");
+        a.ratio_gthr = e ? atoi(e) : 0;
+    }
+    {
         const char *e = getenv("FMPNP_DBG");  // debug knob, read per launch (fmpnp_internal.h LaunchArgs::dbg)
         a.dbg = e ? atoi(e) : 0;
     }

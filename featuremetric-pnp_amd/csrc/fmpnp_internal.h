@@ -72,6 +72,7 @@ struct LaunchArgs {
     // problem; ss_pose [n][24] and ss_rec [n][nc_max][SS_BLK] doubles of granules, sstag | (k + 1)
     // the tag of evaluation k's granules (0xFFFF: the problem is done)
     int ss, ss_cap;               // ss_cap <= SS_CAP: predictions gathered per block per evaluation
+    int ratio_gthr;               // ratio test: the guessed limit after >= this many gathers, else two passes
     double *ss_pose, *ss_rec;
     unsigned long long sstag;
 };

@@ -106,6 +106,7 @@ struct PC {
     int spec_w0;            // the first wave that speculates
     int helpers;            // first-evaluation helper workgroups per problem (0: none)
     int ss_fill;            // steady-state helpers hand records over (a.ss == 1; 2: they only prefetch)
+    int r1;                 // the ratio test of this evaluation takes the guessed limit (else the two passes)
     int hfirst;             // this is the problem's first evaluation
     int prob;               // the problem's index (helpers' record slots)
     const double *hrec;     // the helpers' records [n][nc_max * CH][HREC]
@@ -172,6 +173,9 @@ struct LMState {
     // rstat[b] = max|rho| of block b's supported points (NaN-propagating)
     double rguess[2];
     double rstat[8];
+    // texel gathers of evaluation k (ratio variants): gcnt[k & 1], the next evaluation's choice of
+    // ratio form (a.ratio_gthr)
+    int gcnt[2];
 #if FMPNP_STAMPS
     unsigned long long tlb[NT / 64][16];  // debug timeline (FMPNP_DBG bit 4), flushed at problem end
 #endif
@@ -485,6 +489,7 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
         st.abort_flag = 0;
         st.win_miss = 0;
         st.rguess[0] = st.rguess[1] = INFINITY;  // (evaluation 0: no guess -- every supported point kept)
+        st.gcnt[0] = st.gcnt[1] = 0;
         st.helper_absent = 0;
     }
     __syncthreads();
@@ -1613,7 +1618,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
                      cb % V == 0 && (ce - cb) % V == 0;
     const bool defer = q.use_ratio != 0;
     // (the guessed-limit ratio test: one workgroup per problem of at most 8 blocks)
-    const bool r1 = R1 && defer && q.M <= 8 * 64;
+    const bool r1 = R1 && defer && q.M <= 8 * 64 && q.r1;
     const double rguess = r1 ? ufirst(st.rguess[q.cur_ev & 1]) : 0.0;
     // (a wave below spec_w0 keeps slot 0 and no predictions: the memoised path)
     // (HS with a.ss == 2, the prefetch-only helpers: the main speculates as the _SPEC variants do)
@@ -1725,6 +1730,10 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         if ((q.dbg & 128) && q.cur_ev > 0) m = 0;  // (diagnostics build, FMPNP_DBG bit 7: no gathers after eval 0 -- WRONG results, timing floor only)
 #endif
         ngath += __popcll(m);
+        // (the ratio variants count the evaluation's gathers: the next evaluation's form)
+        if (R1 && defer && m && lane == 0)
+            __hip_atomic_fetch_add(&st.gcnt[q.cur_ev & 1], (int)__popcll(m), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
         if (HELP && q.hfirst && m) {
             // first evaluation with helpers: the block's records at the initial pose come from a
             // helper workgroup (the same gather code at the same pose: identical sums); a point
@@ -2715,8 +2724,14 @@ __device__ __forceinline__ void ss_helper_run(const LaunchArgs &a, int mmax) {
 // test is on, VAR = VAR_GM (Geman-McClure forward, nearest sampling: the common case),
 // VAR_NEAREST (any loss / mode, nearest) or VAR_BILINEAR -- constant-folding the other
 // paths out shortens the per-point code and frees registers.
+// (FMPNP_LAT_WAVES: waves per SIMD the latency build is compiled for -- 2, up to 256 VGPRs; 4 caps it at
+// 128 VGPRs so that two 512-thread workgroups share a CU: the occupancy experiment of DESIGN.md 4.1.4)
+#ifndef FMPNP_LAT_WAVES
+#define FMPNP_LAT_WAVES 2
+#endif
 template <typename T, int WPS, bool TEAM, bool RATIO, int VAR>
-__global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS_WIDE ? 1 : 2) void lm_kernel(LaunchArgs a) {
+__global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
+                             WPS == WPS_WIDE ? 1 : WPS == WPS_LATENCY ? FMPNP_LAT_WAVES : 2) void lm_kernel(LaunchArgs a) {
     LMState &st = S();
     const int G = a.G;
     // XCD-aware team placement: members of one team share blockIdx % gw (the same XCD
@@ -2812,6 +2827,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
                 r.p0 = 0;
             }
             r.use_ratio = RATIO ? 1 : 0;
+            r.r1 = 1;
             r.spec = kSpec ? 1 : 0;
             if constexpr (kSpec) r.no_memo = 0;
             if constexpr (VAR == VAR_GM || VAR == VAR_F_GM || VAR == VAR_GM_SPEC || VAR == VAR_GM_SPEC_H ||
@@ -2842,6 +2858,11 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
             tl_stamp(q, 0);
             q.hfirst = first_eval && q.helpers > 0 && p == team;  // helpers serve each team's first problem
             first_eval = false;
+            // the ratio test's form for this evaluation: the guessed limit after an evaluation that
+            // gathered at least a.ratio_gthr texels (its pass 1 has the slack to hide the early partials),
+            // else the two passes -- both give the same partials bit for bit (ratio_guess_check)
+            if constexpr (kRatio1)
+                q.r1 = (k == 0 || a.ratio_gthr <= 0 || ufirst(st.gcnt[(k + 1) & 1]) >= a.ratio_gthr) ? 1 : 0;
             // project, gather, loss (+ partials)
             // (double-buffered gathers in both builds; speculation in the latency build only)
             // (bilinear: the cell memo; VAR_BIL_DIRECT samples every point at every evaluation)
@@ -2853,16 +2874,21 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT, WPS == WPS
                     q, mmax, ngath, pose);
             // the ratio test: with one workgroup per problem of at most 8 blocks, the guessed limit
             // (ratio_guess_check, after barrier 1); otherwise the two passes (exchange, contrib_pass)
-            const bool r1 = kRatio1 && q.use_ratio && q.M <= 8 * 64;
+            const bool r1 = kRatio1 && q.use_ratio && q.M <= 8 * 64 && q.r1;
             if (q.use_ratio && !r1) {
                 if (!ratio_exchange(lmax)) break;
-                contrib_pass(q, mmax, ufirst(st.rho_max) * st.c.ratio_thr);
+                const double limit = ufirst(st.rho_max) * st.c.ratio_thr;
+                contrib_pass(q, mmax, limit);
+                // (the next evaluation's guess, should it take the guessed form)
+                if (kRatio1 && tid == 0) st.rguess[(k + 1) & 1] = isnan(limit) ? INFINITY : limit;
             }
             const int wave = tid >> 6;
             constexpr bool FLV = VAR == VAR_F_GM || VAR == VAR_F_NEAREST;
             tl_stamp(q, 4);
             if (TEAM) team_arrive();
             else __syncthreads();
+            // (every wave read the previous evaluation's count at this evaluation's start)
+            if (kRatio1 && tid == 0) st.gcnt[(k + 1) & 1] = 0;
             if (r1) {
                 // (FMPNP_DBG bit 5: every block re-formed -- the two-pass partials, for A/B tests;
                 // bit 6: the re-formed blocks counted in texel_gathers' high word)

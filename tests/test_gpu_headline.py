@@ -398,3 +398,23 @@ def test_cfg0_toy_shape_against_oracle(B):
         oracle = list(ex.map(lambda h: oracle_run(h, n_iters=20, loss="squared"), hosts))
     for q in range(B):
         check(res[q], trs[q], *oracle[q], f"toy query {q}")
+
+
+@pytest.mark.parametrize("B,init,ratio", [(128, "easy", 0.8), (128, "hard", 0.8), (16, "easy", 0.5), (1, "hard", 0.8)])
+def test_ratio_form_choice_changes_nothing(B, init, ratio, monkeypatch):
+    """The ratio variants choose per evaluation between the guessed limit and the two passes
+    (FMPNP_RATIO_GTHR: the guess after an evaluation of at least that many texel gathers).  Both
+    forms give the same partials, so any choice gives the same poses, costs, support and kept counts."""
+    probs = [packed_problem(synth.problem_inputs(512, 256, 240, 320, seed=40 + q, device=DEV, init=init))
+             for q in range(B)]
+    o = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, ratio_threshold=ratio, dtype=_lib.F32)
+    monkeypatch.setenv("FMPNP_RATIO_GTHR", "0")  # always the guessed limit
+    base, tb = rf.refine(probs, o, trace=True)
+    for thr in ("1000000000", "20", "1"):  # the two passes after evaluation 0; switching; mostly the guess
+        monkeypatch.setenv("FMPNP_RATIO_GTHR", thr)
+        res, tr = rf.refine(probs, o, trace=True)
+        for q in range(B):
+            assert np.array_equal(res[q]["R"], base[q]["R"]) and np.array_equal(res[q]["t"], base[q]["t"]), (thr, q)
+            assert res[q]["best_cost"] == base[q]["best_cost"] and res[q]["n_evals"] == base[q]["n_evals"], (thr, q)
+            np.testing.assert_array_equal(tr[q]["cost"], tb[q]["cost"])
+            np.testing.assert_array_equal(tr[q]["n_kept"], tb[q]["n_kept"])

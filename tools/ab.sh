@@ -18,10 +18,7 @@ for i in $(seq 1 ${REPS:-3}); do
     python3 - "$name" "gpurun_out/ab_$name.json" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-legs = []
-for k, v in d.items():
-    if isinstance(v, dict) and ("ms_per_launch" in v or "ms_per_refinement" in v or "ms_per_batch" in v):
-        legs.append(f"{k} {v.get('ms_per_launch', v.get('ms_per_refinement', v.get('ms_per_batch')))}")
+legs = [f"{k} {v['ms']}" for k, v in d.get("legs", {}).items() if "ms" in v]  # (the compact line)
 print(f"{sys.argv[1]:>10s}  step {d['ms_per_step']:.4f}  kernel {d['roofline']['avg_kernel_ms']:.4f}  " + "  ".join(legs),
       flush=True)
 PY

@@ -21,7 +21,7 @@ if [ -n "$rev" ]; then
 fi
 rm -f "$out"/*.o "$out/libfmpnp.so"
 pids=""
-for f in fmpnp_lm fmpnp_lm_f32 fmpnp_lm_f64 fmpnp_pack fmpnp_points fmpnp_api; do
+for f in fmpnp_lm fmpnp_lm_f32 fmpnp_lm_f64 fmpnp_pack fmpnp_points fmpnp_query fmpnp_api; do
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -I"$inc" -I"$src" "$@" -c -o "$out/$f.o" "$src/$f.hip" &
   pids="$pids $!"
 done
