@@ -117,9 +117,10 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     // problem on the latency build (a team's waves 4-7 own no block at these sizes).
     int max_span = 0;
     for (int i = 0; i < n; ++i) max_span = std::max(max_span, probs[i].c_end - probs[i].c_begin);
+    static const int spec_maxc = [] { const char *e = getenv("FMPNP_SPEC_MAXC"); return e ? atoi(e) : 0; }();
+    const int maxc = spec_maxc > 0 ? spec_maxc : 64 * (16 / elem_size(opt->dtype));  // (measurement knob)
     P.spec = (FMPNP_SPEC && opt->no_memo == 0 && opt->sampling == FMPNP_NEAREST &&
-              opt->mode == FMPNP_MODE_FORWARD && opt->layout == FMPNP_LAYOUT_FGRAD &&
-              max_span <= 64 * (16 / elem_size(opt->dtype))) ? 1 : 0;
+              opt->mode == FMPNP_MODE_FORWARD && opt->layout == FMPNP_LAYOUT_FGRAD && max_span <= maxc) ? 1 : 0;
     // bilinear sampling keeps each point's cell memo in LDS (at most BIL_MAX_M points per
     // workgroup) unless no_memo asks for every point sampled every evaluation
     const bool bil_memo = opt->sampling == FMPNP_BILINEAR && opt->no_memo != 1;

@@ -166,5 +166,11 @@ hipError_t launch_gather_ref_batch(int n, const void *const *ref, const int *ref
 // per-point 0.5 ||f(p_i) - fref_i||^2 and support at the descriptor's pose (fmpnp_point_costs)
 hipError_t launch_point_costs(const fmpnp_problem &p, int layout, int dtype, double *cost, int *supported,
                               hipStream_t stream);
+// compute_cost (model.py:216-243) at the descriptor's pose: point costs into cost / supported (device,
+// [N] each), then one fixed-order reduction into *out (device): initial_cost, NO_SUPPORT status
+hipError_t launch_compute_cost(const fmpnp_problem &p, int layout, int dtype, int use_ratio, double thr,
+                               double *cost, int *supported, fmpnp_result *out, hipStream_t stream);
+hipError_t launch_cost_mean(const fmpnp_problem &p, int use_ratio, double thr, const double *cost,
+                            const int *supported, fmpnp_result *out, hipStream_t stream);
 
 }  // namespace fmpnp

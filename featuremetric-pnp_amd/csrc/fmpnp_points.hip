@@ -78,4 +78,97 @@ hipError_t launch_point_costs(const fmpnp_problem &p, int layout, int dtype, dou
     return hipGetLastError();
 }
 
+// compute_cost (featurePnP/model.py:216-243) from the per-point costs: ONE workgroup, a fixed
+// summation order (thread t sums points t, t + 256, ... in order, then a fixed tree), so the value
+// depends only on the costs.  With the ratio test the points with |cost| >= max|cost| * thr over the
+// supported ones are dropped (ratio_threshold_feature_errors, model.py:120-129: a NaN maximum keeps
+// none); the mean over none is NaN (torch's mean of an empty tensor).  No supported point: status
+// NO_SUPPORT (the reference returns None, model.py:226-227).
+struct CostMeanArgs {
+    double R[9], t[3];
+    int N, use_ratio;
+    double thr;
+};
+__global__ __launch_bounds__(256) void cost_mean_kernel(const double *__restrict__ cost, const int *__restrict__ sup,
+                                                        CostMeanArgs a, fmpnp_result *__restrict__ out) {
+    __shared__ double sh[256];
+    __shared__ int shn[256];
+    const int t = threadIdx.x;
+    double mx = -1.0;  // (costs are >= 0 or NaN)
+    int ns = 0;
+    for (int i = t; i < a.N; i += 256)
+        if (sup[i]) {
+            ++ns;
+            const double c = fabs(cost[i]);
+            mx = (isnan(c) || isnan(mx)) ? NAN : fmax(mx, c);
+        }
+    sh[t] = mx;
+    shn[t] = ns;
+    __syncthreads();
+    for (int w = 128; w >= 1; w >>= 1) {
+        if (t < w) {
+            const double o = sh[t + w];
+            sh[t] = (isnan(o) || isnan(sh[t])) ? NAN : fmax(sh[t], o);
+            shn[t] += shn[t + w];
+        }
+        __syncthreads();
+    }
+    const double limit = sh[0] * a.thr;
+    const int n_sup = shn[0];
+    __syncthreads();
+    double s = 0.0;
+    int nk = 0;
+    for (int i = t; i < a.N; i += 256)
+        if (sup[i] && (!a.use_ratio || fabs(cost[i]) < limit)) {
+            s += cost[i];
+            ++nk;
+        }
+    sh[t] = s;
+    shn[t] = nk;
+    __syncthreads();
+    for (int w = 128; w >= 1; w >>= 1) {
+        if (t < w) {
+            sh[t] += sh[t + w];
+            shn[t] += shn[t + w];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        fmpnp_result r;
+        for (int k = 0; k < 9; ++k) r.R[k] = a.R[k];
+        for (int k = 0; k < 3; ++k) r.t[k] = a.t[k];
+        r.initial_cost = n_sup ? (shn[0] ? sh[0] / (double)shn[0] : NAN) : NAN;
+        r.best_cost = NAN;
+        r.final_lambda = r.final_lr = NAN;
+        r.best_num_inliers = -1;
+        r.n_evals = 1;
+        r.n_steps = r.n_accepted = 0;
+        r.status = n_sup ? 0 : FMPNP_STATUS_NO_SUPPORT;
+        r.has_best = 0;
+        r.texel_gathers = n_sup;
+        *out = r;
+    }
+}
+
+hipError_t launch_compute_cost(const fmpnp_problem &p, int layout, int dtype, int use_ratio, double thr,
+                               double *cost, int *supported, fmpnp_result *out, hipStream_t stream) {
+    if (p.N > 0) {
+        const hipError_t e = launch_point_costs(p, layout, dtype, cost, supported, stream);
+        if (e != hipSuccess) return e;
+    }
+    return launch_cost_mean(p, use_ratio, thr, cost, supported, out, stream);
+}
+
+hipError_t launch_cost_mean(const fmpnp_problem &p, int use_ratio, double thr, const double *cost,
+                            const int *supported, fmpnp_result *out, hipStream_t stream) {
+    CostMeanArgs a;
+    for (int k = 0; k < 9; ++k) a.R[k] = p.R0[k];
+    for (int k = 0; k < 3; ++k) a.t[k] = p.t0[k];
+    a.N = p.N;
+    a.use_ratio = use_ratio;
+    a.thr = thr;
+    hipLaunchKernelGGL(cost_mean_kernel, dim3(1), dim3(256), 0, stream, cost, supported, a, out);
+    return hipGetLastError();
+}
+
 }  // namespace fmpnp

@@ -80,6 +80,22 @@ int grow(QueryCache &c, int device, size_t dbytes, size_t hbytes) {
 
 }  // namespace
 
+extern "C" int fmpnp_compute_cost_async(const fmpnp_problem *prob, int layout, int dtype, int use_ratio,
+                                        double ratio_threshold, double *cost, int *supported, fmpnp_result *result,
+                                        void *hip_stream) {
+    if (!prob || !result || (prob->N > 0 && (!cost || !supported))) return FMPNP_EINVAL;
+    const fmpnp_problem &p = *prob;
+    if (layout != FMPNP_LAYOUT_FGRAD && layout != FMPNP_LAYOUT_F) return FMPNP_EINVAL;
+    if (dtype != FMPNP_F32 && dtype != FMPNP_F64) return FMPNP_EINVAL;
+    if (layout == FMPNP_LAYOUT_F && dtype != FMPNP_F32) return FMPNP_EINVAL;
+    if (p.N < 0 || p.c_end <= p.c_begin) return FMPNP_EINVAL;
+    if (p.N > 0) {
+        const int rc = fmpnp_point_costs(prob, layout, dtype, cost, supported, hip_stream);  // (validates the rest)
+        if (rc) return rc;
+    }
+    return (int)launch_cost_mean(p, use_ratio, ratio_threshold, cost, supported, result, (hipStream_t)hip_stream);
+}
+
 extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, int H, int W, const void *ref_chw,
                                  int dtype_ref, int C_ref, int H_ref, int W_ref, const double *ref_inliers,
                                  const double *pts3d, int N, const double K[9], const double R0[9], const double t0[3],
@@ -106,9 +122,6 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
     // host-side descriptors: [0] compute_cost over the whole map (levels only), then the forwards
     fmpnp_problem hd[1 + 64];
     if (n_res > 65) return FMPNP_EINVAL;
-    fmpnp_options oc = *opt;
-    oc.mode = FMPNP_MODE_COMPUTE_COST;  // model.py:216-243: squared, the whole channel range
-    oc.loss = FMPNP_SQUARED;
     for (int r = 0; r < n_res; ++r) {
         fmpnp_problem &p = hd[r];
         memset(&p, 0, sizeof(p));
@@ -131,8 +144,8 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
     }
     // the LM workspace of the largest plan (the launches run one after another on the stream)
     size_t ws = 0;
-    for (int r = 0; r < n_res; ++r) {
-        const size_t w = fmpnp_workspace_size(&hd[r], 1, (n_levels > 0 && r == 0) ? &oc : opt);
+    for (int r = n_levels > 0 ? 1 : 0; r < n_res; ++r) {  // (compute_cost: point costs + one reduction)
+        const size_t w = fmpnp_workspace_size(&hd[r], 1, opt);
         if (w == 0) return FMPNP_EINVAL;  // (fmpnp_workspace_size: invalid problem / options)
         ws = std::max(ws, w);
     }
@@ -142,8 +155,9 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
     const size_t b_res = al(sizeof(fmpnp_result) * n_res), b_err = 256;
     const size_t b_tr = trace ? al(sizeof(fmpnp_trace_entry) * (size_t)n_fwd * stride) : 0;
     const size_t b_feat = al((size_t)H * W * planes * cs * es), b_fref = al((size_t)std::max(N, 1) * cs * es);
+    const size_t b_cost = n_levels > 0 ? al((size_t)std::max(N, 1) * 12) : 0;  // compute_cost's per-point costs
     const size_t up = b_inl + b_pts + b_desc, down = b_res + b_err + b_tr;
-    const size_t need = up + down + b_feat + b_fref + al(ws);
+    const size_t need = up + down + b_feat + b_fref + al(ws) + b_cost;
 
     hipStream_t s = (hipStream_t)hip_stream;
     std::lock_guard<std::mutex> lock(g_q.mu);
@@ -159,6 +173,8 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
     int *d_err = (int *)(d + up + b_res);
     fmpnp_trace_entry *d_tr = trace ? (fmpnp_trace_entry *)(d + up + b_res + b_err) : nullptr;
     unsigned char *d_feat = d + up + down, *d_fref = d_feat + b_feat, *d_ws = d_fref + b_fref;
+    double *d_cost = (double *)(d_ws + al(ws));
+    int *d_sup = (int *)(d_cost + std::max(N, 1));
     for (int r = 0; r < n_res; ++r) {
         hd[r].feat = d_feat;
         hd[r].fref = d_fref;
@@ -200,6 +216,14 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
     // the LM launches
     for (int r = 0; r < n_res; ++r) {
         const bool cost = n_levels > 0 && r == 0;
+        if (cost) {
+            // compute_cost (model.py:216-243): every point's cost at once (one wave each), one
+            // fixed-order reduction -- one evaluation, so not an LM launch (a latency chain there)
+            e = launch_compute_cost(hd[0], opt->layout, opt->dtype, opt->use_ratio, opt->ratio_threshold, d_cost, d_sup,
+                                    d_res, s);
+            if (e != hipSuccess) return (int)e;
+            continue;
+        }
         if (n_levels > 0 && r >= 2) {
             // level r - 1 starts from level r - 2's result: R[9], t[3] -> R0[9], t0[3] (contiguous)
             static_assert(offsetof(fmpnp_problem, t0) == offsetof(fmpnp_problem, R0) + 72, "R0, t0 contiguous");
@@ -210,8 +234,7 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
             if (e != hipSuccess) return (int)e;
         }
         fmpnp_trace_entry *tr = (trace && !cost) ? d_tr + (size_t)(n_levels > 0 ? r - 1 : 0) * stride : nullptr;
-        rc = fmpnp_refine_batch_async(d_desc + r, &hd[r], 1, N, cost ? &oc : opt, d_res + r, tr, stride, d_ws, ws,
-                                      hip_stream);
+        rc = fmpnp_refine_batch_async(d_desc + r, &hd[r], 1, N, opt, d_res + r, tr, stride, d_ws, ws, hip_stream);
         if (rc) return rc;
     }
     // the one download

@@ -155,8 +155,9 @@ class sparseFeaturePnP(nn.Module):
     def _compute_cost_packed(self, feats, pts3D, R, t, feature_ref, K, im_width, im_height, c_begin=0, c_end=None):
         prob = _rf.make_problem(feats, feature_ref, pts3D, _to_np(K, (3, 3)), im_width, im_height, _to_np(R, (3, 3)),
                                 _to_np(t, (3,)), c_begin, c_end)
-        opts = self._options(feats.dtype_code, _lib.MODE_COMPUTE_COST, loss=_lib.SQUARED)
-        (res,), _ = _rf.refine([prob], opts)
+        # one evaluation: per-point costs + one fixed-order reduction (fmpnp_compute_cost_async), the
+        # same kernels as the one-call façade's multilevel path
+        res = _rf.compute_cost(prob, self.use_ratio_test_, self.ratio_threshold_)
         if res["status"] & _lib.STATUS_NO_SUPPORT:
             return None
         return torch.tensor(res["initial_cost"], dtype=torch.float64)

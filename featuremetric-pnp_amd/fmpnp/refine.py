@@ -420,6 +420,26 @@ def point_costs(problem, R=None, t=None):
     return cost, sup.bool()
 
 
+def compute_cost(problem, use_ratio=False, ratio_threshold=0.0):
+    """compute_cost (featurePnP/model.py:216-243) at the problem's (R0, t0) on the device:
+    fmpnp_compute_cost_async (per-point costs, one fixed-order reduction).  Returns the result
+    dict (initial_cost; status NO_SUPPORT when no point is supported)."""
+    p = problem.descriptor()
+    dev = problem.feats.buf.device
+    N = int(p.N)
+    cost = torch.empty(max(N, 1), dtype=torch.float64, device=dev)
+    sup = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
+    res = torch.empty(RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    lay = _lib.LAYOUT_F if problem.feats.layout == "f" else _lib.LAYOUT_FGRAD
+    with torch.cuda.device(dev):
+        rc = _lib.load().fmpnp_compute_cost_async(ctypes.byref(p), lay, problem.feats.dtype_code, int(bool(use_ratio)),
+                                                  float(ratio_threshold or 0.0), ctypes.c_void_p(cost.data_ptr()),
+                                                  ctypes.c_void_p(sup.data_ptr()), ctypes.c_void_p(res.data_ptr()),
+                                                  _lib.stream_ptr(dev))
+    _lib.check(rc, "fmpnp_compute_cost_async")
+    return results_from_array(res.cpu().numpy().view(RESULT_DTYPE))[0]
+
+
 def project_pixels(R, t, pts3d, K):
     """Host restatement of the pixel projection (model.py:303-308) for track_['points2d'];
     elementwise numpy (no FMA), matching the device's sequential fp64 arithmetic."""

@@ -235,6 +235,16 @@ int fmpnp_gather_reference_batch(int n, const void *const *ref_chw, const int *r
 int fmpnp_point_costs(const fmpnp_problem *prob, int layout, int dtype, double *cost, int *supported,
                       void *hip_stream);
 
+/* compute_cost (featurePnP/model.py:216-243) at the descriptor's pose (R0, t0): the mean over the
+ * supported points -- after the ratio test when use_ratio (model.py:230-236) -- of
+ * 0.5 ||f(p_i) - fref_i||^2 over [c_begin, c_end).  fmpnp_point_costs (one wave per point) into
+ * cost / supported (DEVICE [N] fp64 / int32 scratch), then one fixed-order reduction into *result
+ * (DEVICE): initial_cost (NaN when the ratio test keeps nothing), status FMPNP_STATUS_NO_SUPPORT when
+ * no point is supported (the reference returns None), R / t = (R0, t0).  The descriptor is host
+ * memory; asynchronous on hip_stream.  One evaluation: it is not an LM launch. */
+int fmpnp_compute_cost_async(const fmpnp_problem *prob, int layout, int dtype, int use_ratio, double ratio_threshold,
+                             double *cost, int *supported, fmpnp_result *result, void *hip_stream);
+
 /* Device workspace needed by fmpnp_refine_batch_async for n problems (team exchange slots and,
  * for small batches, the first-evaluation helpers' records; no initialisation needed, reusable
  * by later launches on the same stream). */
