@@ -762,9 +762,11 @@ def facade_calls(dev, synth, name, calls=24, warmup=2, via="feature_pnp", querie
         t, quat, model = fmpnp.optimize_feature_pnp(q[None], _StubNet(r), pr, K, image_shape=img, feature_pyramid=pyr,
                                                     model=model)
         return model
+    from fmpnp import _lib
     for i in range(warmup):
         one(i)
     torch.cuda.synchronize()
+    reruns0 = _lib.load().fmpnp_feature_pnp_reruns()
     t0 = time.perf_counter()
     statuses = set()
     for i in range(calls):
@@ -772,7 +774,9 @@ def facade_calls(dev, synth, name, calls=24, warmup=2, via="feature_pnp", querie
         statuses.add(int(m.status_ or 0))
     dt = time.perf_counter() - t0
     N, Cq, H, W = FACADE_SHAPES[name][:4]
+    reruns = _lib.load().fmpnp_feature_pnp_reruns() - reruns0
     return {"ms_per_call": round(dt / calls * 1e3, 4), "calls_per_s": round(calls / dt, 1), "calls": calls,
+            "window_reruns": int(reruns),
             "distinct_queries": len(batch), "statuses": sorted(statuses), "via": via,
             "shape": f"N={N} C={Cq} {H}x{W}" + (" pyramid default_robotcar.gin:75" if pyr else "")}
 

@@ -43,8 +43,9 @@ int validate_problem(const fmpnp_problem &p, int layout, int sampling) {
     if (p.c_begin < 0 || p.c_end < p.c_begin || p.c_end > p.cstride || p.c_end > p.ld_ref) return FMPNP_EINVAL;
     if (p.N > 0 && (!p.feat || !p.fref || !p.pts3d)) return FMPNP_EINVAL;
     if (layout == FMPNP_LAYOUT_F && (p.Hf >= 65536 || p.Wf >= 65536)) return FMPNP_ETOOBIG;
-    // a packed window (fmpnp_pack_features_f_window_batch) is read by the f-only layout's gathers only
-    if (p.window && layout != FMPNP_LAYOUT_F) return FMPNP_EINVAL;
+    // a packed window (fmpnp_pack_features_f_window_batch, fmpnp_feature_pnp) is read by nearest
+    // sampling's gathers only
+    if (p.window && sampling != FMPNP_NEAREST) return FMPNP_EINVAL;
     // bilinear cell keys pack (row + 1, column + 1) into 15 + 16 bits
     if (sampling == FMPNP_BILINEAR && (p.Hf >= 32768 || p.Wf >= 65535)) return FMPNP_ETOOBIG;
     // the packed map must hold 3*cstride per texel
@@ -119,7 +120,11 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     for (int i = 0; i < n; ++i) max_span = std::max(max_span, probs[i].c_end - probs[i].c_begin);
     static const int spec_maxc = [] { const char *e = getenv("FMPNP_SPEC_MAXC"); return e ? atoi(e) : 0; }();
     const int maxc = spec_maxc > 0 ? spec_maxc : 64 * (16 / elem_size(opt->dtype));  // (measurement knob)
-    P.spec = (FMPNP_SPEC && opt->no_memo == 0 && opt->sampling == FMPNP_NEAREST &&
+    // packed windows (fmpnp_feature_pnp, the windowed f-only packs): the speculative gathers would read
+    // predicted texels outside the window, so they are off
+    bool windows = false;
+    for (int i = 0; i < n; ++i) windows = windows || probs[i].window != nullptr;
+    P.spec = (FMPNP_SPEC && !windows && opt->no_memo == 0 && opt->sampling == FMPNP_NEAREST &&
               opt->mode == FMPNP_MODE_FORWARD && opt->layout == FMPNP_LAYOUT_FGRAD && max_span <= maxc) ? 1 : 0;
     // bilinear sampling keeps each point's cell memo in LDS (at most BIL_MAX_M points per
     // workgroup) unless no_memo asks for every point sampled every evaluation
@@ -176,10 +181,9 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     G = std::min(G, MAX_G);
     // packed windows: one workgroup per problem (a window miss stops the problem inside its
     // workgroup, fmpnp_lm_impl.h eval_pass; a team would wait on the stopped member)
-    bool windows = false;
-    for (int i = 0; i < n; ++i) windows = windows || probs[i].window != nullptr;
-    if (windows) G = 1;
-    while (!windows && G < std::min(P.nc_max, MAX_G) && !fits(G)) ++G;
+    // (packed f, gx, gy planes: the miss is only flagged and the problem finishes, so teams stay)
+    if (windows && opt->layout == FMPNP_LAYOUT_F) G = 1;
+    while (!(windows && opt->layout == FMPNP_LAYOUT_F) && G < std::min(P.nc_max, MAX_G) && !fits(G)) ++G;
     if (!fits(G)) return FMPNP_ETOOBIG;
     P.G = G;
     P.mmax = ((P.nc_max + G - 1) / G) * CH;

@@ -150,6 +150,12 @@ hipError_t launch_pack(const void *chw, const void *gx, const void *gy, int dtyp
                        int dtype_out, int cs, int normalized, int replicate, hipStream_t stream, int planes = 3);
 hipError_t launch_gather_ref(const void *ref, int dtype_in, int C, int H, int W, const double *inl, int N, int img0,
                              int img1, void *out, int dtype_out, int ld_out, int *err, hipStream_t stream);
+// the window map of n problems ([2][Hf][Wf] bytes at fmpnp_problem.window): cleared, then every point's
+// square of `radius` texels around its texel at (R0, t0) marked in plane 0 (radius - 1 in plane 1)
+hipError_t launch_win_mark(const fmpnp_problem *probs_dev, int n, int radius, int max_n, long max_hw, hipStream_t stream);
+// fused Sobel + channels-last pack of the texels marked in win ([H][W] bytes, plane 0) only
+hipError_t launch_pack_win(const void *chw, int dtype_in, int C, int H, int W, void *out, int dtype_out, int cs,
+                           int normalized, int replicate, const unsigned char *win, hipStream_t stream);
 // n f-only packs (FMPNP_LAYOUT_F, fp32 out) in ceil(n / 32) launches; shape[4i..] = C, H, W, cstride
 hipError_t launch_pack_f_batch(int n, const void *const *chw, void *const *out, const int *shape, int dtype_in,
                                hipStream_t stream);

@@ -69,7 +69,7 @@ struct Ctx {
     double *part_g;       // [2][nc_max][NV] of this team
     double *max_g;        // [2][G] of this team
     double lambda0, ratio_thr, alpha;
-    int mode, n_iters, use_ratio, loss, G, s, trace_stride, nc_max, no_memo, sampling, sobel_flags;
+    int mode, n_iters, use_ratio, loss, G, s, trace_stride, nc_max, no_memo, sampling, sobel_flags, layout;
     int spec;             // speculative gathers of the predicted next texels (memoised nearest modes)
     int spec_cap;         // ... at most this many per wave per evaluation
     int spec_w0;          // ... by the waves >= spec_w0
@@ -448,7 +448,9 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
         c.feat = pb->feat;
         c.fref = pb->fref;
         c.pts = pb->pts3d;
-        c.win_ok = pb->window ? pb->window + (size_t)pb->Hf * pb->Wf : nullptr;
+        // the texels a gather may read: plane 1 (the whole 3x3 neighbourhood packed) for the f-only
+        // layout's in-gather Sobel, plane 0 (the texel packed) for the packed f, gx, gy planes
+        c.win_ok = pb->window ? pb->window + (c.layout == FMPNP_LAYOUT_F ? (size_t)pb->Hf * pb->Wf : 0) : nullptr;
         c.N = pb->N;
         c.Hf = pb->Hf;
         c.Wf = pb->Wf;
@@ -527,8 +529,8 @@ __device__ __forceinline__ void problem_end(bool own_gathers, int k, unsigned lo
 #endif
     if (threadIdx.x == 0) {
         LMScal &sc = st.sc[k & 1];
-        if (st.abort_flag && st.win_miss) {
-            sc.status |= FMPNP_STATUS_WINDOW;  // (one workgroup per problem: nothing else to stop)
+        if (st.win_miss) {
+            sc.status |= FMPNP_STATUS_WINDOW;  // (f-only layout: one workgroup per problem, nothing else to stop)
         } else if (st.abort_flag) {
             st.c.dead = 1;
             sc.status |= FMPNP_STATUS_SYNC_TIMEOUT;
@@ -547,13 +549,17 @@ __device__ __forceinline__ void problem_end(bool own_gathers, int k, unsigned lo
             r.n_evals = sc.n_evals;
             r.n_steps = sc.n_steps;
             r.n_accepted = sc.n_accepted;
-            r.status = sc.status;
+            // (a team's results were zeroed: every member ORs in its window misses, below)
+            if (st.c.G > 1) atomicOr(&r.status, sc.status);
+            else r.status = sc.status;
             r.has_best = sc.has_best;
             if (own_gathers) {
                 long long g = 0;
                 for (int w = 0; w < nwaves(); ++w) g += st.wg_gath[w];
                 r.texel_gathers = g;
             }
+        } else if (st.win_miss) {
+            atomicOr(&st.c.results[st.c.p].status, FMPNP_STATUS_WINDOW);  // (another team member's miss)
         }
     }
     __syncthreads();
@@ -1709,10 +1715,15 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
             }
         }
         unsigned long long m = __ballot(dirty);
-        if constexpr (FL) {
-            // packed window (fmpnp_pack_features_f_window_batch): every texel gathered must have its
-            // 3x3 neighbourhood packed; a miss stops the problem after this evaluation (abort_flag is
-            // read only after barriers) with FMPNP_STATUS_WINDOW, its result invalid
+        // (not in the speculating variants: the planner never gives them a window, and the check costs
+        // the headline 1 % -- profiles/r05_window_check_ab.txt)
+        if constexpr (FL || !SP) {
+            // packed window (fmpnp_pack_features_f_window_batch; fmpnp_feature_pnp's windowed packs):
+            // every texel gathered must be packed -- for the f-only layout its whole 3x3 neighbourhood.
+            // A miss is never read; it marks the problem's result invalid (FMPNP_STATUS_WINDOW: the
+            // caller packs in full and refines again).  The f-only layout stops the problem after this
+            // evaluation (abort_flag, read only after barriers: one workgroup per problem); the packed
+            // layout finishes it (a team's members never wait on a stopped one)
             const unsigned char *wok = ufirst(st.c.win_ok);
             if (wok != nullptr && m) {
                 const bool miss = ((m >> lane) & 1ull) && wok[off] == 0;
@@ -1721,7 +1732,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
                     m &= ~mm;  // (never read an unpacked texel)
                     if (lane == 0) {
                         st.win_miss = 1;
-                        st.abort_flag = 1;
+                        if (FL) st.abort_flag = 1;
                     }
                 }
             }
@@ -2769,6 +2780,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
         c.dbg = a.dbg;
         c.sampling = a.opt.sampling;
         c.sobel_flags = a.opt.sobel_flags;
+        c.layout = a.opt.layout;
         c.stamps_on = a.stamps != nullptr && !(a.dbg & 20);  // dbg bit 2 / 4: per-evaluation stamps / timeline instead
         c.G = G;
         c.s = s;

@@ -241,9 +241,11 @@ __device__ __forceinline__ void sb_put(Tout v, __amdgpu_buffer_rsrc_t rsrc, int 
 //   Tin = float : separable form, column sums then differences (6 fp64 ops per texel); exact
 //                 in fp64 for fp32 inputs, so the rounded result is the oracle's.
 //   Tin = double: the oracle's association (helpers/sobel_pytorch.py:9-59 order), bit-equal.
-template <typename Tin, typename Tout, bool FULL, bool NORM, bool NTS, bool GRAD>
+// WIN: wmask bit k = column k of the wave's run is marked in the packed window (the others are not
+// written: the LM never reads them, fmpnp_feature_pnp's windowed pack)
+template <typename Tin, typename Tout, bool FULL, bool NORM, bool NTS, bool GRAD, bool WIN = false>
 __device__ __forceinline__ void sb_row(const Tin *rm, const Tin *r0, const Tin *rp, __amdgpu_buffer_rsrc_t rsrc,
-                                       int voff, int soff0, int tstride, int pstride, int ncols) {
+                                       int voff, int soff0, int tstride, int pstride, int ncols, unsigned wmask = 0) {
     constexpr double sc = NORM ? 0.125 : 1.0;
     if constexpr (sizeof(Tin) == 4) {
         // column j: sx_j = a_j + 2 d_j + g_j (for gx), sy_j = g_j - a_j (for gy)
@@ -257,7 +259,7 @@ __device__ __forceinline__ void sb_row(const Tin *rm, const Tin *r0, const Tin *
             const double a2 = rm[k + 2], d2 = r0[k + 2], g2 = rp[k + 2];
             const double sxp = (a2 + 2.0 * d2) + g2, syp = g2 - a2;
             const double gx = sxp - sxm, gy = (sym + 2.0 * sy0) + syp;
-            if (FULL || k < ncols) {
+            if ((FULL || k < ncols) && (!WIN || ((wmask >> k) & 1u))) {
                 const int so = soff0 + k * tstride;
                 sb_put<Tout, NTS>((Tout)f0, rsrc, voff, so);
                 if constexpr (GRAD) {
@@ -275,7 +277,7 @@ __device__ __forceinline__ void sb_row(const Tin *rm, const Tin *r0, const Tin *
             // cross-correlation with kx = [[-1,0,1],[-2,0,2],[-1,0,1]], ky = kx^T, oracle order
             const double gx = ((-a0 + a2) + (-2.0 * d0 + 2.0 * d2)) + (-g0 + g2);
             const double gy = ((-a0 - 2.0 * a1) - a2) + ((g0 + 2.0 * g1) + g2);
-            if (FULL || k < ncols) {
+            if ((FULL || k < ncols) && (!WIN || ((wmask >> k) & 1u))) {
                 const int so = soff0 + k * tstride;
                 sb_put<Tout, NTS>((Tout)d1, rsrc, voff, so);
                 if constexpr (GRAD) {
@@ -289,10 +291,10 @@ __device__ __forceinline__ void sb_row(const Tin *rm, const Tin *r0, const Tin *
 }
 
 // FAST: 16-B vector loads (aligned rows) and all 32 tile columns inside the map.
-template <typename Tin, typename Tout, bool NORM, bool NTS, bool FAST, bool GRAD>
+template <typename Tin, typename Tout, bool NORM, bool NTS, bool FAST, bool GRAD, bool WIN = false>
 __device__ __forceinline__ void sobel_pack_body(const Tin *__restrict__ chw, int C, int H, int W, int cs, int rs,
                                                 int replicate, Tin *ring, __amdgpu_buffer_rsrc_t rsrc, int c0, int x0,
-                                                int y0, int dir) {
+                                                int y0, int dir, const unsigned char *__restrict__ win = nullptr) {
     constexpr int SE = SB_CB * SB_LD;
     const int y1 = min(y0 + rs, H);
     const int cc = threadIdx.x & 63, run = threadIdx.x >> 6;
@@ -330,17 +332,25 @@ __device__ __forceinline__ void sobel_pack_body(const Tin *__restrict__ chw, int
             const Tin *r0 = ring + (y & 3) * SE + lo;
             const Tin *rp = ring + ((y + 1) & 3) * SE + lo;
             const int soff0 = ((y - y0) * W + x0 + wrun * SB_RUN) * tstride;
-            sb_row<Tin, Tout, FAST, NORM, NTS, GRAD>(rm, r0, rp, rsrc, voff_s, soff0, tstride, pstride, ncols);
+            unsigned wm = 0;
+            if constexpr (WIN) {  // the run's marks (wave-uniform bytes)
+                const unsigned char *wr = win + (size_t)y * W + x0 + wrun * SB_RUN;
+#pragma unroll
+                for (int k = 0; k < SB_RUN; ++k) wm |= (k < ncols && wr[k]) ? (1u << k) : 0u;
+            }
+            if (!WIN || wm)
+                sb_row<Tin, Tout, FAST, NORM, NTS, GRAD, WIN>(rm, r0, rp, rsrc, voff_s, soff0, tstride, pstride, ncols,
+                                                              wm);
         }
         if (more) sb_store<Tin>(r, ring + ((y + 2 * dir) & 3) * SE);
     }
 }
 
-template <typename Tin, typename Tout, bool NORM, bool NTS, bool GRAD>
+template <typename Tin, typename Tout, bool NORM, bool NTS, bool GRAD, bool WIN = false>
 __global__ __launch_bounds__(SB_NT) void sobel_pack_kernel(const Tin *__restrict__ chw, int C, int H, int W,
                                                         Tout *__restrict__ out, int cs, int rs, int replicate,
                                                         int vec_ok, int ncb, int nxw, int ntiles, int xcd_map,
-                                                        int alt_dir) {
+                                                        int alt_dir, const unsigned char *__restrict__ win = nullptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Tin *ring = reinterpret_cast<Tin *>(smem);  // [SB_SLOTS][SB_CB][SB_LD]
     // Tile order: channel chunk fastest, then column block, then row block.  xcd_map: the
@@ -362,20 +372,31 @@ __global__ __launch_bounds__(SB_NT) void sobel_pack_kernel(const Tin *__restrict
     const int c0 = cb * SB_CB, x0 = xb * SB_XW, y0 = yb * rs;
     const int dir = (alt_dir && (yb & 1)) ? -1 : 1;
     const int y1 = min(y0 + rs, H);
+    if constexpr (WIN) {  // a tile without a marked texel: nothing read, nothing written
+        int any = 0;
+        for (int e = threadIdx.x; e < (y1 - y0) * SB_XW; e += SB_NT) {
+            const int yy = y0 + e / SB_XW, xx = x0 + e % SB_XW;
+            any |= (xx < W && win[(size_t)yy * W + xx]) ? 1 : 0;
+        }
+        if (!__syncthreads_or(any)) return;
+    }
     // descriptor over this tile's output rows [y0, y1) x all columns (byte offsets < 2^31)
     const size_t texel_elems = (size_t)(GRAD ? 3 : 1) * cs;
     Tout *tile_base = out + (size_t)y0 * W * texel_elems;
     const unsigned tile_bytes = (unsigned)((size_t)(y1 - y0) * W * texel_elems * sizeof(Tout));
     __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_base, 0, tile_bytes, 0x00020000);
     if (vec_ok && x0 + SB_XW <= W)
-        sobel_pack_body<Tin, Tout, NORM, NTS, true, GRAD>(chw, C, H, W, cs, rs, replicate, ring, rsrc, c0, x0, y0, dir);
+        sobel_pack_body<Tin, Tout, NORM, NTS, true, GRAD, WIN>(chw, C, H, W, cs, rs, replicate, ring, rsrc, c0, x0, y0,
+                                                               dir, win);
     else
-        sobel_pack_body<Tin, Tout, NORM, NTS, false, GRAD>(chw, C, H, W, cs, rs, replicate, ring, rsrc, c0, x0, y0, dir);
+        sobel_pack_body<Tin, Tout, NORM, NTS, false, GRAD, WIN>(chw, C, H, W, cs, rs, replicate, ring, rsrc, c0, x0, y0,
+                                                                dir, win);
 }
 
 template <typename Tin, typename Tout>
 static hipError_t pack_t(const void *chw, const void *gx, const void *gy, int C, int H, int W, void *out, int cs,
-                         int normalized, int replicate, bool grad, hipStream_t stream) {
+                         int normalized, int replicate, bool grad, hipStream_t stream,
+                         const unsigned char *win = nullptr) {
     if (gx) {
         dim3 grid((C + PK_CB - 1) / PK_CB, (W + PK_XW - 1) / PK_XW, (H + PK_RS - 1) / PK_RS);
         size_t lds = 3 * PK_CB * PK_LD * sizeof(Tin);
@@ -402,6 +423,18 @@ static hipError_t pack_t(const void *chw, const void *gx, const void *gy, int C,
     // nt stores by default (the packed map is streamed out once; measured 2-17 % faster than
     // plain stores over cfg2..cfg5 shapes); FMPNP_PACK_NT=0 selects plain stores
     static const int nts = [] { const char *e = getenv("FMPNP_PACK_NT"); return !(e && *e == '0'); }();
+    if (win) {  // windowed (fmpnp_feature_pnp): the marked texels only, nt stores
+        if (!grad) return hipErrorInvalidValue;
+        if (normalized)
+            hipLaunchKernelGGL((sobel_pack_kernel<Tin, Tout, true, true, true, true>), grid, dim3(SB_NT), lds, stream,
+                               (const Tin *)chw, C, H, W, (Tout *)out, cs, rs, replicate, vec_ok, ncb, nxw, ntiles,
+                               xcd_map, alt_dir, win);
+        else
+            hipLaunchKernelGGL((sobel_pack_kernel<Tin, Tout, false, true, true, true>), grid, dim3(SB_NT), lds, stream,
+                               (const Tin *)chw, C, H, W, (Tout *)out, cs, rs, replicate, vec_ok, ncb, nxw, ntiles,
+                               xcd_map, alt_dir, win);
+        return hipGetLastError();
+    }
 #define SB_LAUNCH(NORM, NTS, GRAD)                                                                              \
     hipLaunchKernelGGL((sobel_pack_kernel<Tin, Tout, NORM, NTS, GRAD>), grid, dim3(SB_NT), lds, stream,        \
                        (const Tin *)chw, C, H, W, (Tout *)out, cs, rs, replicate, vec_ok, ncb, nxw, ntiles, xcd_map, alt_dir)
@@ -774,6 +807,30 @@ hipError_t launch_pack_f_window(const fmpnp_problem *probs_dev, const fmpnp_prob
     case 6: return pack_f_window_tiles<64, 128>(probs_dev, probs_host, n, chw, dtype_in, stream);
     default: return pack_f_window_tiles<64, 32>(probs_dev, probs_host, n, chw, dtype_in, stream);
     }
+}
+
+hipError_t launch_win_mark(const fmpnp_problem *probs_dev, int n, int radius, int max_n, long max_hw, hipStream_t stream) {
+    const unsigned ny = (unsigned)n;
+    const unsigned cb = (unsigned)std::min<long>((2 * max_hw + 16L * PK_NT - 1) / (16L * PK_NT), 1024);
+    hipLaunchKernelGGL(win_clear_kernel, dim3(std::max(cb, 1u), ny), dim3(PK_NT), 0, stream, probs_dev);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || max_n <= 0) return e;
+    const long nt = (long)max_n * (2 * radius + 1);
+    hipLaunchKernelGGL(win_mark_kernel, dim3((unsigned)((nt + PK_NT - 1) / PK_NT), ny), dim3(PK_NT), 0, stream, probs_dev,
+                       radius);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_win(const void *chw, int dtype_in, int C, int H, int W, void *out, int dtype_out, int cs,
+                           int normalized, int replicate, const unsigned char *win, hipStream_t stream) {
+    if (!win) return hipErrorInvalidValue;
+    if (dtype_in == FMPNP_F32 && dtype_out == FMPNP_F32)
+        return pack_t<float, float>(chw, nullptr, nullptr, C, H, W, out, cs, normalized, replicate, true, stream, win);
+    if (dtype_in == FMPNP_F32 && dtype_out == FMPNP_F64)
+        return pack_t<float, double>(chw, nullptr, nullptr, C, H, W, out, cs, normalized, replicate, true, stream, win);
+    if (dtype_in == FMPNP_F64 && dtype_out == FMPNP_F32)
+        return pack_t<double, float>(chw, nullptr, nullptr, C, H, W, out, cs, normalized, replicate, true, stream, win);
+    return pack_t<double, double>(chw, nullptr, nullptr, C, H, W, out, cs, normalized, replicate, true, stream, win);
 }
 
 hipError_t launch_pack(const void *chw, const void *gx, const void *gy, int dtype_in, int C, int H, int W, void *out,

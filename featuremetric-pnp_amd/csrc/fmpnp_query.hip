@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 
 #include "fmpnp.h"
@@ -44,6 +45,7 @@ struct QueryCache {
     size_t host_bytes = 0;
 };
 QueryCache g_q;
+std::atomic<long long> g_window_reruns{0};  // fmpnp_feature_pnp calls re-run fully packed after a window miss
 
 int grow(QueryCache &c, int device, size_t dbytes, size_t hbytes) {
     if (c.dev && (c.dev_bytes < dbytes || c.device != device)) {
@@ -100,8 +102,8 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
                                  int dtype_ref, int C_ref, int H_ref, int W_ref, const double *ref_inliers,
                                  const double *pts3d, int N, const double K[9], const double R0[9], const double t0[3],
                                  int img0, int img1, const fmpnp_level *levels, int n_levels,
-                                 const fmpnp_options *opt, fmpnp_result *results, fmpnp_trace_entry *trace,
-                                 int trace_stride, void *hip_stream) {
+                                 const fmpnp_options *opt, int window_radius, fmpnp_result *results,
+                                 fmpnp_trace_entry *trace, int trace_stride, void *hip_stream) {
     if (!query_chw || !ref_chw || !opt || !results || !K || !R0 || !t0 || N < 0 || C <= 0 || H <= 0 || W <= 0 ||
         C_ref != C || H_ref <= 0 || W_ref <= 0 || img0 <= 0 || img1 <= 0 || n_levels < 0 || (n_levels > 0 && !levels))
         return FMPNP_EINVAL;
@@ -109,6 +111,10 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
     if ((dtype_query != FMPNP_F32 && dtype_query != FMPNP_F64) || (dtype_ref != FMPNP_F32 && dtype_ref != FMPNP_F64))
         return FMPNP_EINVAL;
     if (opt->mode != FMPNP_MODE_FORWARD || (trace && trace_stride < 1)) return FMPNP_EINVAL;
+    // packed windows: the fused Sobel pack of the packed f, gx, gy planes, nearest sampling
+    if (window_radius < 0 || window_radius > 4096 ||
+        (window_radius > 0 && (opt->layout != FMPNP_LAYOUT_FGRAD || opt->sampling != FMPNP_NEAREST)))
+        return FMPNP_EINVAL;
     for (int l = 0; l < n_levels; ++l)
         if (levels[l].c_begin < 0 || levels[l].c_end <= levels[l].c_begin || levels[l].c_end > C) return FMPNP_EINVAL;
     const bool lay_f = opt->layout == FMPNP_LAYOUT_F;
@@ -143,12 +149,16 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
         p.pts3d = (const double *)(uintptr_t)256;
     }
     // the LM workspace of the largest plan (the launches run one after another on the stream)
+    // (with and without the window: a window miss re-runs the call fully packed)
     size_t ws = 0;
-    for (int r = n_levels > 0 ? 1 : 0; r < n_res; ++r) {  // (compute_cost: point costs + one reduction)
-        const size_t w = fmpnp_workspace_size(&hd[r], 1, opt);
-        if (w == 0) return FMPNP_EINVAL;  // (fmpnp_workspace_size: invalid problem / options)
-        ws = std::max(ws, w);
-    }
+    for (int wi = 0; wi < (window_radius > 0 ? 2 : 1); ++wi)
+        for (int r = n_levels > 0 ? 1 : 0; r < n_res; ++r) {  // (compute_cost: point costs + one reduction)
+            fmpnp_problem pw = hd[r];
+            pw.window = wi ? (const unsigned char *)(uintptr_t)256 : nullptr;
+            const size_t w = fmpnp_workspace_size(&pw, 1, opt);
+            if (w == 0) return FMPNP_EINVAL;  // (fmpnp_workspace_size: invalid problem / options)
+            ws = std::max(ws, w);
+        }
     // device carve: [inl | pts | descs] (the one upload), [results | err | trace] (the one
     // download), the packed map, fref, the LM workspace
     const size_t b_inl = al((size_t)N * 16), b_pts = al((size_t)N * 24), b_desc = al(sizeof(fmpnp_problem) * n_res);
@@ -157,7 +167,8 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
     const size_t b_feat = al((size_t)H * W * planes * cs * es), b_fref = al((size_t)std::max(N, 1) * cs * es);
     const size_t b_cost = n_levels > 0 ? al((size_t)std::max(N, 1) * 12) : 0;  // compute_cost's per-point costs
     const size_t up = b_inl + b_pts + b_desc, down = b_res + b_err + b_tr;
-    const size_t need = up + down + b_feat + b_fref + al(ws) + b_cost;
+    const size_t b_win = window_radius > 0 ? al((size_t)2 * H * W) : 0;  // [2][H][W] window map
+    const size_t need = up + down + b_feat + b_fref + al(ws) + b_cost + b_win;
 
     hipStream_t s = (hipStream_t)hip_stream;
     std::lock_guard<std::mutex> lock(g_q.mu);
@@ -175,11 +186,17 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
     unsigned char *d_feat = d + up + down, *d_fref = d_feat + b_feat, *d_ws = d_fref + b_fref;
     double *d_cost = (double *)(d_ws + al(ws));
     int *d_sup = (int *)(d_cost + std::max(N, 1));
+    unsigned char *d_win = (unsigned char *)d_cost + b_cost;
     for (int r = 0; r < n_res; ++r) {
         hd[r].feat = d_feat;
         hd[r].fref = d_fref;
         hd[r].pts3d = d_pts;
     }
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    // attempt 0: windowed when asked; attempt 1 (only after a window miss): the full pack
+    const bool win = attempt == 0 && window_radius > 0;
+    if (attempt == 1 && window_radius == 0) break;
+    for (int r = 0; r < n_res; ++r) hd[r].window = win ? d_win : nullptr;
     // the one upload
     if (N > 0) {
         memcpy(h, ref_inliers, (size_t)N * 16);
@@ -200,8 +217,18 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
         e = hipMemsetAsync(d_feat, 0, b_feat, s);
         if (e != hipSuccess) return (int)e;
     }
-    e = launch_pack(query_chw, nullptr, nullptr, dtype_query, C, H, W, d_feat, opt->dtype, cs, opt->sobel_flags & 1,
-                    (opt->sobel_flags >> 1) & 1, s, planes);
+    if (win) {
+        // only the texels within window_radius of a point's texel at (R0, t0) (its square in plane 0 of
+        // the window map): the refinement reads the texels its points visit, a few from where they
+        // start; the LM flags a gather outside the window (FMPNP_STATUS_WINDOW) and the call re-runs
+        e = launch_win_mark(d_desc, 1, window_radius, N, (long)H * W, s);
+        if (e != hipSuccess) return (int)e;
+        e = launch_pack_win(query_chw, dtype_query, C, H, W, d_feat, opt->dtype, cs, opt->sobel_flags & 1,
+                            (opt->sobel_flags >> 1) & 1, d_win, s);
+    } else {
+        e = launch_pack(query_chw, nullptr, nullptr, dtype_query, C, H, W, d_feat, opt->dtype, cs,
+                        opt->sobel_flags & 1, (opt->sobel_flags >> 1) & 1, s, planes);
+    }
     if (e != hipSuccess) return (int)e;
     // fref (optimize_feature_pnp.py:51-56): the reference map's first C channels
     if (N > 0) {
@@ -242,8 +269,18 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
     if (e != hipSuccess) return (int)e;
     e = hipStreamSynchronize(s);
     if (e != hipSuccess) return (int)e;
+    bool miss = false;
+    for (int r = 0; r < n_res; ++r) miss = miss || (((const fmpnp_result *)h)[r].status & FMPNP_STATUS_WINDOW);
+    if (win && miss) {
+        g_window_reruns.fetch_add(1);
+        continue;  // a point left its window: every result of this attempt is invalid
+    }
     memcpy(results, h, sizeof(fmpnp_result) * n_res);
     if (trace) memcpy(trace, h + b_res + b_err, sizeof(fmpnp_trace_entry) * (size_t)n_fwd * stride);
     const int err = *(const int *)(h + b_res);
     return err ? FMPNP_ERANGE : 0;
+  }
+    return FMPNP_EINVAL;  // (not reached)
 }
+
+extern "C" long long fmpnp_feature_pnp_reruns(void) { return g_window_reruns.load(); }

@@ -78,7 +78,8 @@ EXPORTS = ["fmpnp_abi_version", "fmpnp_build_info", "fmpnp_device_check", "fmpnp
            "fmpnp_gather_reference", "fmpnp_gather_reference_async", "fmpnp_pack_features_batch", "fmpnp_pack_features_f",
            "fmpnp_gather_reference_batch", "fmpnp_workspace_size", "fmpnp_refine_batch_async", "fmpnp_refine_batch",
            "fmpnp_last_launch", "fmpnp_debug_stamps", "fmpnp_plan", "fmpnp_last_launch_info",
-           "fmpnp_pack_features_f_window_batch", "fmpnp_feature_pnp", "fmpnp_compute_cost_async"]
+           "fmpnp_pack_features_f_window_batch", "fmpnp_feature_pnp", "fmpnp_compute_cost_async",
+           "fmpnp_feature_pnp_reruns"]
 
 _LIB = None
 
@@ -135,8 +136,10 @@ def load():
     L.fmpnp_compute_cost_async.restype = i
     dp = ctypes.POINTER(ctypes.c_double)
     L.fmpnp_feature_pnp.argtypes = [vp, i, i, i, i, vp, i, i, i, i, vp, vp, i, dp, dp, dp, i, i,
-                                    ctypes.POINTER(Level), i, ctypes.POINTER(Options), vp, vp, i, vp]
+                                    ctypes.POINTER(Level), i, ctypes.POINTER(Options), i, vp, vp, i, vp]
     L.fmpnp_feature_pnp.restype = i
+    if hasattr(L, "fmpnp_feature_pnp_reruns"):  # (A/B builds of earlier sources lack it)
+        L.fmpnp_feature_pnp_reruns.restype = ctypes.c_longlong
     if L.fmpnp_abi_version() != ABI_VERSION:
         raise FmpnpError("libfmpnp ABI mismatch")
     _LIB = L

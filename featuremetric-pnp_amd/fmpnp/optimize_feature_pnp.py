@@ -7,6 +7,8 @@ LM loop on the CPU (optimize_feature_pnp.py:51-69).  Here the query hypercolumn
 stays on the device: one fused Sobel + channels-last pack kernel, one gather
 kernel for the reference descriptors, one LM launch.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -57,14 +59,18 @@ def feature_pnp_multi(query_hypercolumns, reference_hypercolumns, prediction, K,
 
 
 def feature_pnp(query_hypercolumns, reference_hypercolumns, prediction, K, image_shape, track=False,
-                feature_pyramid=None, model=None, storage=None, layout=None):
+                feature_pyramid=None, model=None, storage=None, layout=None, window=None):
     """optimize_feature_pnp.py:50-71.  Returns (R, t, model) with R, t fp64 CPU tensors.
 
     layout: None (default) packs the f/gx/gy planes ("fgrad": the fused Sobel + channels-last
     pack); "f" packs f only (FMPNP_LAYOUT_F: a third of the pack's bytes, the LM kernel forms
     the fp64 Sobel gradients of every texel it gathers).  One query per call is LM-bound, and
     the LM reads 16C bytes per gathered texel from "fgrad" against 40C from "f": cfg2, one
-    call, pack + LM 66 + 259 us against 33 + 559 us (rocprofv3, profiles/r05_facade_*)."""
+    call, pack + LM 66 + 259 us against 33 + 559 us (rocprofv3, profiles/r05_facade_*).
+
+    window: the one-call path packs only the texels within `window` texels of each point's texel
+    at the initial pose (fmpnp_feature_pnp; a point that leaves its window re-runs the call fully
+    packed, so results are the full pack's bit for bit); None = window_radius(C, H, W, N), 0 = off."""
     model = _new_model(model)
     q = query_hypercolumns[0] if query_hypercolumns.dim() == 4 else query_hypercolumns
     dev = q.device if q.is_cuda else torch.device("cuda", torch.cuda.current_device())
@@ -74,7 +80,7 @@ def feature_pnp(query_hypercolumns, reference_hypercolumns, prediction, K, image
     levels = _channel_levels(feature_pyramid, q.shape[0])
     if _one_call_ok(model, q, reference_hypercolumns, feature_pyramid, levels, track, storage, layout):
         return _feature_pnp_one_call(model, q, reference_hypercolumns, prediction, K, image_shape, track, levels,
-                                     storage, layout)
+                                     storage, layout, window)
     feats = _rf.pack_features(q, storage=storage, device=dev, layout=layout)               # :57, :61
     fref = _rf.gather_reference(reference_hypercolumns, prediction.reference_inliers, image_shape,
                                 cstride=feats.cstride, storage=storage, device=dev)          # :51-56
@@ -118,7 +124,19 @@ def _one_call_ok(model, q, r, feature_pyramid, levels, track, storage, layout):
     return ok
 
 
-def _feature_pnp_one_call(model, q, r, prediction, K, image_shape, track, levels, storage, layout):
+def window_radius(C, H, W, N):
+    """The one-call path's default pack window (texels): FMPNP_FACADE_WINDOW overrides."""
+    env = os.environ.get("FMPNP_FACADE_WINDOW")
+    if env is not None:
+        return int(env)
+    # wide maps only: the windowed pack saves the writes of the unmarked texels (RobotCar C = 1664 at
+    # 256x256, 295 / 866 points: 1.57 -> 1.42 / 1.97 -> 1.88 ms per call), but a window turns the
+    # speculative gathers off (cfg2, C = 256: 0.450 -> 0.465 ms); radius 6: no re-run over the
+    # synthetic starts at radii >= 5 (profiles/r05_facade_window_sweep.txt)
+    return 6 if C > 256 else 0
+
+
+def _feature_pnp_one_call(model, q, r, prediction, K, image_shape, track, levels, storage, layout, window=None):
     """feature_pnp through fmpnp_feature_pnp: one host call, one host wait (optimize_feature_pnp.py:50-71)."""
     import ctypes
     from . import _lib
@@ -138,6 +156,10 @@ def _feature_pnp_one_call(model, q, r, prediction, K, image_shape, track, levels
     Kn = np.ascontiguousarray((K.detach().cpu().numpy() if isinstance(K, torch.Tensor) else np.asarray(K))
                               .astype(np.float64).reshape(3, 3))
     n_lv = len(levels) if levels else 0
+    if window is None:
+        window = window_radius(C, H, W, pts.shape[0])
+    if layout != "fgrad" or getattr(model, "sampling", "nearest") != "nearest":
+        window = 0
     lv = (_lib.Level * max(n_lv, 1))(*[_lib.Level(a, b) for a, b in (levels or [])])
     res = np.zeros(n_lv + 1 if n_lv else 1, dtype=_rf.RESULT_DTYPE)
     want_trace = bool(track) or bool(model.verbose)
@@ -150,7 +172,7 @@ def _feature_pnp_one_call(model, q, r, prediction, K, image_shape, track, levels
             vp(q.data_ptr()), _rf._dtype_code(q.dtype), C, H, W, vp(r.data_ptr()), _rf._dtype_code(r.dtype),
             r.shape[0], r.shape[1], r.shape[2], vp(inl.ctypes.data), vp(pts.ctypes.data), pts.shape[0],
             Kn.ctypes.data_as(dp), R0.ctypes.data_as(dp), t0.ctypes.data_as(dp), int(image_shape[0]),
-            int(image_shape[1]), lv if n_lv else None, n_lv, ctypes.byref(opts), vp(res.ctypes.data), tr,
+            int(image_shape[1]), lv if n_lv else None, n_lv, ctypes.byref(opts), int(window), vp(res.ctypes.data), tr,
             stride if want_trace else 0, _lib.stream_ptr(dev))
     if rc == _lib.ERANGE:
         raise IndexError("a reference inlier maps outside the reference hypercolumn "

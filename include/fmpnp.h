@@ -140,7 +140,9 @@ typedef struct {
                                        texel whose whole 3x3 neighbourhood is packed.  The LM kernel checks
                                        plane 1 at every gather and stops the problem with
                                        FMPNP_STATUS_WINDOW on a miss, so a result without that bit equals the
-                                       fully packed map's bit for bit. */
+                                       fully packed map's bit for bit.  FMPNP_LAYOUT_FGRAD (nearest
+                                       sampling; fmpnp_feature_pnp's windowed packs): plane 0 is checked,
+                                       and a miss only sets FMPNP_STATUS_WINDOW (the problem finishes). */
 } fmpnp_problem;
 
 typedef struct {
@@ -290,7 +292,14 @@ int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, int H, int 
                       int dtype_ref, int C_ref, int H_ref, int W_ref, const double *ref_inliers,
                       const double *pts3d, int N, const double K[9], const double R0[9], const double t0[3],
                       int img0, int img1, const fmpnp_level *levels, int n_levels, const fmpnp_options *opt,
-                      fmpnp_result *results, fmpnp_trace_entry *trace, int trace_stride, void *hip_stream);
+                      int window_radius, fmpnp_result *results, fmpnp_trace_entry *trace, int trace_stride,
+                      void *hip_stream);
+/* window_radius > 0 (FMPNP_LAYOUT_FGRAD, nearest sampling): pack only the texels within that many texels
+ * (Chebyshev) of a point's texel at (R0, t0) -- the refinement reads the texels its points visit, a
+ * few from where they start.  An LM gather outside the window marks the attempt invalid and the call
+ * runs again fully packed, so the results are the full pack's bit for bit either way.  0: full pack.
+ * fmpnp_feature_pnp_reruns(): how many calls of this process ran again after a window miss. */
+long long fmpnp_feature_pnp_reruns(void);
 
 /* Debug: when device_buf != NULL, later LM launches write per-workgroup phase cycle
  * totals (s_memtime) to device_buf[grid][8 waves][12] (8 phases, then the first evaluation's

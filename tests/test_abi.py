@@ -158,12 +158,12 @@ def test_feature_pnp_call_rejects_bad_arguments_without_a_device():
     o = _lib.Options()
     res = (_lib.Result * 4)()
 
-    def call(q=4096, C=8, Cr=8, lv=None, nlv=0, opt=o, res_=res, dq=0, N=4):
+    def call(q=4096, C=8, Cr=8, lv=None, nlv=0, opt=o, res_=res, dq=0, N=4, win=0):
         arr = (_lib.Level * max(nlv, 1))(*(lv or []))
         return L.fmpnp_feature_pnp(vp(q) if q else None, dq, C, 16, 16, vp(4096), 0, Cr, 16, 16,
                                    vp(inl.ctypes.data), vp(pts.ctypes.data), N, K.ctypes.data_as(dp),
                                    K.ctypes.data_as(dp), K[:3].ctypes.data_as(dp), 64, 64,
-                                   arr if nlv else None, nlv, ctypes.byref(opt), res_, None, 0, None)
+                                   arr if nlv else None, nlv, ctypes.byref(opt), win, res_, None, 0, None)
     assert call(q=0) == -1                                   # no query map
     assert call(Cr=9) == -1                                  # reference map of another channel count
     assert call(dq=3) == -1                                  # unknown dtype
@@ -174,3 +174,7 @@ def test_feature_pnp_call_rejects_bad_arguments_without_a_device():
     oc = _lib.Options.from_buffer_copy(o)
     oc.mode = _lib.MODE_COMPUTE_COST
     assert call(opt=oc) == -1                                # forward only (compute_cost runs inside)
+    assert call(win=-1) == -1                                # a negative window radius
+    of = _lib.Options.from_buffer_copy(o)
+    of.layout = _lib.LAYOUT_F
+    assert call(opt=of, win=5) == -1                         # windows: the packed f, gx, gy planes only

@@ -146,3 +146,32 @@ def test_one_call_no_support_returns_initial_pose_for_pyramids(monkeypatch):
     assert out[0][2].initial_cost_ is None and out[1][2].initial_cost_ is None
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
     np.testing.assert_array_equal(out[0][1].numpy(), T[:3, 3])
+
+
+@pytest.mark.parametrize("shape,pyr,init", [((512, 256, 240, 320), None, "easy"),
+                                            ((295, 384, 64, 64), [(128, 384, None, None), (0, 128, None, None)],
+                                             "easy"),
+                                            ((900, 192, 96, 96), [(64, 192, None, None), (0, 64, None, None)],
+                                             "hard")])
+def test_windowed_one_call_equals_full_pack(shape, pyr, init, monkeypatch):
+    """fmpnp_feature_pnp with a packed window (only the texels near each point's initial texel are
+    packed; a gather outside it re-runs the call fully packed) gives the full pack's results bit for
+    bit -- at a radius that fits, and at radius 1 where points leave their windows (the re-run path);
+    N = 900 (15 blocks) runs as a team of workgroups."""
+    from fmpnp import _lib
+    N, C, H, W = shape
+    (batch,), img = synth.pipeline_queries(1, 1, N, C, H, W, device=DEV, seed0=21, init=init)
+    q, r, p, K = batch[0]
+    pred = Pred(p.points_3d, p.reference_inliers, p.matrix, np.array([1.0, 0, 0, 0]), "ref.png")
+
+    def run(win):
+        model = fmpnp.sparseFeaturePnP(50, loss_fn=fmpnp.geman_mcclure_loss, lambda_=0.01, storage=torch.float32)
+        return _run(True, monkeypatch, q[None], r, pred, K, img, track=True, feature_pyramid=pyr, model=model,
+                    window=win)
+    full = run(0)
+    L = _lib.load()
+    for win in (6, 1):
+        before = L.fmpnp_feature_pnp_reruns()
+        _same(run(win), full)
+        if win == 1 and N >= 512:
+            assert L.fmpnp_feature_pnp_reruns() > before  # (the points of these starts move > 1 texel)
