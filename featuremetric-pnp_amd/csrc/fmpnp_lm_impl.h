@@ -69,7 +69,7 @@ struct Ctx {
     double *part_g;       // [2][nc_max][NV] of this team
     double *max_g;        // [2][G] of this team
     double lambda0, ratio_thr, alpha;
-    int mode, n_iters, use_ratio, loss, G, s, trace_stride, nc_max, no_memo, sampling, sobel_flags, layout;
+    int mode, n_iters, use_ratio, loss, G, s, trace_stride, nc_max, no_memo, sampling, sobel_flags;
     int spec;             // speculative gathers of the predicted next texels (memoised nearest modes)
     int spec_cap;         // ... at most this many per wave per evaluation
     int spec_w0;          // ... by the waves >= spec_w0
@@ -87,6 +87,7 @@ struct Ctx {
     float txpx, typx, pxtx, pypx;  // texels per image pixel, image pixels per texel (x, y)
     UDiv div_h, div_w;    // exact floor division by im_h, im_w (indexing_)
     int p0, M, c0, LC, NC;
+    int layout;           // fmpnp_layout of the launch (the window plane a gather checks)
 };
 
 // Per-problem constants of the point phases, held in registers (every value wave-uniform:
@@ -550,7 +551,7 @@ __device__ __forceinline__ void problem_end(bool own_gathers, int k, unsigned lo
             r.n_steps = sc.n_steps;
             r.n_accepted = sc.n_accepted;
             // (a team's results were zeroed: every member ORs in its window misses, below)
-            if (st.c.G > 1) atomicOr(&r.status, sc.status);
+            if (!own_gathers) atomicOr(&r.status, sc.status);
             else r.status = sc.status;
             r.has_best = sc.has_best;
             if (own_gathers) {
@@ -558,7 +559,7 @@ __device__ __forceinline__ void problem_end(bool own_gathers, int k, unsigned lo
                 for (int w = 0; w < nwaves(); ++w) g += st.wg_gath[w];
                 r.texel_gathers = g;
             }
-        } else if (st.win_miss) {
+        } else if (!own_gathers && st.win_miss) {
             atomicOr(&st.c.results[st.c.p].status, FMPNP_STATUS_WINDOW);  // (another team member's miss)
         }
     }

@@ -121,6 +121,9 @@ class RefinePipeline:
         if self.window is not None and (self.layout != "f" or self.window < 2):
             raise ValueError("window needs the f-only layout and a radius >= 2")
         self.refills = 0  # queries re-run with the full pack after leaving their window
+        # host seconds (perf_counter) in preparing batches (of which the first batch's: nothing
+        # runs on the device yet), collecting results while streaming, and the final drain
+        self.host_s = {"prepare": 0.0, "first_prepare": 0.0, "finish": 0.0, "drain": 0.0}
         self.unwindowed_batches = 0  # batches packed in full: a problem too large for a windowed plan
         self.levels = [tuple(int(c) for c in lv) for lv in levels] if levels else None
         if self.levels and self.window is not None:
@@ -190,10 +193,12 @@ class RefinePipeline:
                     slab[int(starts[i]):int(starts[i] + sizes[i])].zero_()
             # one out-of-map flag per query, read once the batch finished (no host wait here)
             err = torch.zeros(nq, dtype=torch.int32, device=dev)
-            # every query's reference inliers and 3D points in one pinned upload
-            flat = np.concatenate([a.reshape(-1) for a in inl + pts])
-            dflat = torch.from_numpy(flat).pin_memory().to(dev, non_blocking=True)
+            # every query's reference inliers and 3D points in one pinned upload (written straight into
+            # pinned memory: one host copy)
             offs = np.concatenate([[0], np.cumsum([a.size for a in inl + pts])])
+            pinned = torch.empty(int(offs[-1]), dtype=torch.float64, pin_memory=True)
+            np.concatenate([a.reshape(-1) for a in inl + pts], out=pinned.numpy())
+            dflat = pinned.to(dev, non_blocking=True)
             # reference descriptors of the whole batch: [N_i][cstride_i] runs in one buffer
             pad = any(int(css[i]) != rmaps[i].shape[0] for i in range(nq))
             fbuf = (torch.zeros if pad else torch.empty)(max(int(fr_off[-1]), 1), dtype=storage, device=dev)
@@ -320,12 +325,19 @@ class RefinePipeline:
                 raise _lib.FmpnpError(f"batch {len(out)}: cross-workgroup exchange timed out")
             out.append(res)
 
+        import time
         for i, queries in enumerate(batches):
             # the host stays at most `depth` batches ahead of the collected results
             while len(inflight) >= self.depth:
+                t0 = time.perf_counter()
                 finish(inflight.pop(0))
+                self.host_s["finish"] += time.perf_counter() - t0
             k = i % self.depth
+            t0 = time.perf_counter()
             batch, keep, err = self._prepare(list(queries), k)
+            self.host_s["prepare"] += time.perf_counter() - t0
+            if i == 0:
+                self.host_s["first_prepare"] += time.perf_counter() - t0
             ready = torch.cuda.Event()
             ready.record(self.prep)
             self.solve.wait_event(ready)
@@ -340,6 +352,8 @@ class RefinePipeline:
             self.slab_free[k] = done
             inflight.append((batch, keep, err, done))
             del batch, keep, err
+        t0 = time.perf_counter()
         for entry in inflight:
             finish(entry)
+        self.host_s["drain"] += time.perf_counter() - t0
         return out

@@ -137,13 +137,19 @@ def test_validation_errors():
 
 
 def test_windowed_problems_plan_one_workgroup(monkeypatch):
-    """A packed window (fmpnp_problem.window) forces one workgroup per problem (a window miss
-    stops the problem inside its workgroup), and is refused outside the f-only layout."""
+    """A packed window (fmpnp_problem.window) on the f-only layout forces one workgroup per problem
+    (a window miss stops the problem inside its workgroup); on the packed f/gx/gy planes a miss is
+    only flagged, so the plan keeps its workgroups but drops the speculative gathers (they would read
+    predicted texels outside the window); bilinear sampling refuses windows."""
     o = rf.make_options(**GM)
     o.layout = _lib.LAYOUT_F
     i = plan(1, o)
     assert i["wgs_per_problem"] > 1  # (a single f-only problem spreads over CUs)
     i = plan(1, o, window=True)
     assert i["wgs_per_problem"] == 1 and i["team"] == 0
+    i = plan(128, rf.make_options(**GM))
+    assert i["speculate"] == 1 and i["variant_name"] == "GM_SPEC"
+    i = plan(128, rf.make_options(**GM), window=True)
+    assert i["speculate"] == 0 and i["variant_name"] == "GM"
     with pytest.raises(_lib.FmpnpError):
-        plan(1, rf.make_options(**GM), window=True)
+        plan(1, rf.make_options(**dict(GM, sampling="bilinear")), window=True)

@@ -13,6 +13,11 @@ done
 [ -f "$P/pipeline/summary.json" ] && cp "$P/pipeline/summary.json" "profiles/${R}_pmc_pipeline.json"
 [ -f "$P/pipeline_w5/summary.json" ] && cp "$P/pipeline_w5/summary.json" "profiles/${R}_pmc_pipeline_w5.json"
 [ -f "$P/pipeline_robotcar/summary.json" ] && cp "$P/pipeline_robotcar/summary.json" "profiles/${R}_pmc_pipeline_robotcar.json"
+for d in "$P"/facade_*/; do
+  t=$(basename "$d")
+  [ -f "$d/summary.json" ] && cp "$d/summary.json" "profiles/${R}_pmc_$t.json"
+  [ -f "$d/kernel_stats.csv" ] && cp "$d/kernel_stats.csv" "profiles/${R}_rocprof_kernel_stats_$t.csv"
+done
 for n in 866 295; do
   [ -f "$P/pyramid_n$n/summary.json" ] && cp "$P/pyramid_n$n/summary.json" "profiles/${R}_pmc_pyramid_n$n.json"
 done

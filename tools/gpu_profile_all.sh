@@ -21,6 +21,7 @@ timeout -k 10 400 bash tools/gpu_profile_pipeline.sh > gpurun_out/prof_pipe.log 
 ROBOTCAR=1 timeout -k 10 400 bash tools/gpu_profile_pipeline.sh > gpurun_out/prof_pipe_robotcar.log 2>&1 || exit 1
 timeout -k 10 400 bash tools/gpu_profile_pyramid.sh 866 > gpurun_out/prof_pyr866.log 2>&1 || exit 1
 timeout -k 10 400 bash tools/gpu_profile_pyramid.sh 295 > gpurun_out/prof_pyr295.log 2>&1 || exit 1
+timeout -k 10 500 bash tools/gpu_profile_facade.sh > gpurun_out/prof_facade.log 2>&1 || exit 1
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 -s KILL 120 rocprofv3 --pmc TA_TA_BUSY_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE --output-format csv \
     -d "$GRAFT_REPO_ROOT/gpurun_out/prof/tatd" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --legs none --steps 5 \
