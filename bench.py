@@ -833,8 +833,7 @@ def pipeline_leg(dev, synth):
                 runs += rep
                 if rep == 1:
                     res, refills = r, max(refills, pipe.refills - before)
-        timed.host_ms = {k: round(v / runs * 1e3 * (nb if k != "first_prepare" else 1) / nb, 4)
-                         for k, v in pipe.host_s.items()}
+        timed.host_ms = {k: round(v / runs * 1e3, 4) for k, v in pipe.host_s.items()}
         return nb * qb / best[1], best, res, refills
 
     qps, best, res, refills = timed(PIPE_WINDOW, steady=True)

@@ -20,7 +20,7 @@ NB = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 64
 dev = torch.device("cuda", 0)
 batches, img = synth.pipeline_queries(NB, B, device=dev)
-pipe = RefinePipeline(img, storage=torch.float32, depth=2,
+pipe = RefinePipeline(img, storage=torch.float32, depth=2, window=int(os.environ.get("WINDOW", "0")) or None,
                       model_kwargs=dict(n_iters=50, loss_fn=fmpnp.geman_mcclure_loss, lambda_=0.01,
                                         ratio_threshold=None))
 pipe.run(batches)
