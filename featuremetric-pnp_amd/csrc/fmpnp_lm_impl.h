@@ -87,7 +87,6 @@ struct Ctx {
     float txpx, typx, pxtx, pypx;  // texels per image pixel, image pixels per texel (x, y)
     UDiv div_h, div_w;    // exact floor division by im_h, im_w (indexing_)
     int p0, M, c0, LC, NC;
-    int layout;           // fmpnp_layout of the launch (the window plane a gather checks)
 };
 
 // Per-problem constants of the point phases, held in registers (every value wave-uniform:
@@ -449,9 +448,7 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
         c.feat = pb->feat;
         c.fref = pb->fref;
         c.pts = pb->pts3d;
-        // the texels a gather may read: plane 1 (the whole 3x3 neighbourhood packed) for the f-only
-        // layout's in-gather Sobel, plane 0 (the texel packed) for the packed f, gx, gy planes
-        c.win_ok = pb->window ? pb->window + (c.layout == FMPNP_LAYOUT_F ? (size_t)pb->Hf * pb->Wf : 0) : nullptr;
+        c.win_ok = pb->window ? pb->window + (size_t)pb->Hf * pb->Wf : nullptr;
         c.N = pb->N;
         c.Hf = pb->Hf;
         c.Wf = pb->Wf;
@@ -1720,14 +1717,15 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         // the headline 1 % -- profiles/r05_window_check_ab.txt)
         if constexpr (FL || !SP) {
             // packed window (fmpnp_pack_features_f_window_batch; fmpnp_feature_pnp's windowed packs):
-            // every texel gathered must be packed -- for the f-only layout its whole 3x3 neighbourhood.
-            // A miss is never read; it marks the problem's result invalid (FMPNP_STATUS_WINDOW: the
-            // caller packs in full and refines again).  The f-only layout stops the problem after this
-            // evaluation (abort_flag, read only after barriers: one workgroup per problem); the packed
-            // layout finishes it (a team's members never wait on a stopped one)
+            // every texel gathered must be packed -- for the f-only layout its whole 3x3 neighbourhood
+            // (plane 1, st.c.win_ok), for the packed f, gx, gy planes the texel itself (plane 0, Hf * Wf
+            // bytes before).  A miss is never read; it marks the problem's result invalid
+            // (FMPNP_STATUS_WINDOW: the caller packs in full and refines again).  The f-only layout stops
+            // the problem after this evaluation (abort_flag, read only after barriers: one workgroup per
+            // problem); the packed layout finishes it (a team's members never wait on a stopped one)
             const unsigned char *wok = ufirst(st.c.win_ok);
             if (wok != nullptr && m) {
-                const bool miss = ((m >> lane) & 1ull) && wok[off] == 0;
+                const bool miss = ((m >> lane) & 1ull) && wok[FL ? off : off - q.Hf * q.Wf] == 0;
                 const unsigned long long mm = __ballot(miss);
                 if (mm) {
                     m &= ~mm;  // (never read an unpacked texel)
@@ -2781,7 +2779,6 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
         c.dbg = a.dbg;
         c.sampling = a.opt.sampling;
         c.sobel_flags = a.opt.sobel_flags;
-        c.layout = a.opt.layout;
         c.stamps_on = a.stamps != nullptr && !(a.dbg & 20);  // dbg bit 2 / 4: per-evaluation stamps / timeline instead
         c.G = G;
         c.s = s;
