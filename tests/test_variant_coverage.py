@@ -57,7 +57,8 @@ RECIPES = {
     "gm_h":             (1, "gm", "fwd", "nearest", "fgrad", True, False, 0, "GM_H", "latency", 0),
     "nearest":          (128, "cauchy", "fwd", "nearest", "fgrad", True, False, 0, "NEAREST", "latency", 0),
     "nearest_h":        (1, "cauchy", "fwd", "nearest", "fgrad", True, False, 0, "NEAREST_H", "latency", 0),
-    "compute_cost":     (1, "gm", "cost", "nearest", "fgrad", True, True, 0, "NEAREST", "latency", 0),
+    # (compute_cost is one all-points evaluation: the planner keeps the team spread at B=1)
+    "compute_cost":     (1, "gm", "cost", "nearest", "fgrad", True, True, 0, "NEAREST", "latency", 1),
     "bil_direct":       (1, "gm", "fwd", "bilinear", "fgrad", False, False, 1, "BIL_DIRECT", "latency", 0),
     "f_gm":             (1, "gm", "fwd", "nearest", "f", True, True, 1, "F_GM", "latency", 0),
     "f_nearest":        (1, "cauchy", "fwd", "nearest", "f", True, True, 1, "F_NEAREST", "latency", 0),
