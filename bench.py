@@ -37,6 +37,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
        rank 0 prints the line.  Under a launcher (WORLD_SIZE set) --gpus must equal WORLD_SIZE.
 """
 import argparse
+import gc
 import json
 import math
 import os
@@ -551,9 +552,15 @@ def fixed_total_leg(args, dev, probs, feats, inputs, opts, rf, synth, stream, op
     from fmpnp import _lib
     n = 1024
     torch.cuda.synchronize()
+    # the earlier legs' pipelines and façade buffers (reference cycles: freed by the collector)
+    gc.collect()
+    torch.cuda.empty_cache()
     free, _ = torch.cuda.mem_get_info(dev)
     need = (n - len(probs)) * (HF * WF * 3 * C * 4 + N_PTS * C * 4 + N_PTS * 24) + (8 << 30)
     layout = args.layout if free > need else "f"
+    if layout != args.layout:
+        print(f"[bench] fixed_total_1024: {free / 2**30:.1f} GiB free < {need / 2**30:.1f} GiB needed for the "
+              f"{args.layout} layout: f-only layout", file=sys.stderr)
     if layout != args.layout:
         probs, feats = [], []
     ps = list(probs)
@@ -571,7 +578,8 @@ def fixed_total_leg(args, dev, probs, feats, inputs, opts, rf, synth, stream, op
         d = leg_summary(workload_tag(n, args.init, args.ratio, memo, args.sampling, layout), ms, r, n,
                         args.sampling, layout)
         d.update(layout=layout, launch=_lib.last_launch(),
-                 resident_GiB=round(torch.cuda.memory_allocated(dev) / 2**30, 1))
+                 resident_GiB=round(torch.cuda.memory_allocated(dev) / 2**30, 1),
+                 free_GiB_before=round(free / 2**30, 1), packed_need_GiB=round(need / 2**30, 1))
         out["fixed_total_1024"] = d
     note = ("1024 queries resident: >= 2 GB of distinct texels per launch, beyond the 256 MB Infinity Cache "
             "(HBM-streamed)")
@@ -833,18 +841,17 @@ def pipeline_leg(dev, synth):
                 runs += rep
                 if rep == 1:
                     res, refills = r, max(refills, pipe.refills - before)
-        timed.host_ms = {k: round(v / runs * 1e3, 4) for k, v in pipe.host_s.items()}
-        return nb * qb / best[1], best, res, refills
+        host_ms = {k: round(v / runs * 1e3, 4) for k, v in pipe.host_s.items()}
+        return nb * qb / best[1], best, res, refills, host_ms
 
-    qps, best, res, refills = timed(PIPE_WINDOW, steady=True)
-    host_ms = timed.host_ms
-    fqps, fbest, fres, _ = timed(None)
+    qps, best, res, refills, host_ms = timed(PIPE_WINDOW, steady=True)
+    fqps, fbest, fres, _, _ = timed(None)
     d8 = best[2] - best[1]
     steady = nb * qb / d8 if d8 > 0.05 * best[1] else None  # (no figure from a difference within noise)
     same = all(np.array_equal(a["R"], b["R"]) and np.array_equal(a["t"], b["t"]) and a["best_cost"] == b["best_cost"]
                for x, y in zip(res, fres) for a, b in zip(x, y))
     hard, _ = synth.pipeline_queries(nb, qb, N_PTS, C, HF, WF, device=dev, seed0=5000, init="hard")
-    hqps, hbest, _, hrefills = timed(PIPE_WINDOW, batches=hard)
+    hqps, hbest, _, hrefills, _ = timed(PIPE_WINDOW, batches=hard)
     del hard
     out = {"queries_per_s": round(qps, 1), "ms_per_query": round(best[1] / (nb * qb) * 1e3, 4),
            "batches": nb, "batch": qb, "statuses": sorted({r["status"] for b in res for r in b}),
@@ -859,7 +866,7 @@ def pipeline_leg(dev, synth):
     out["roofline"] = pipeline_roofline(qps, PIPE_WINDOW)
     out["full_pack"] = {"queries_per_s": round(fqps, 1), "ms_per_query": round(fbest[1] / (nb * qb) * 1e3, 4),
                         "roofline": pipeline_roofline(fqps, None)}
-    del batches
+    del batches, timed  # (timed's defaults hold the batches too)
     out["robotcar_1664"] = robotcar_pipeline_leg(dev, synth)
     return out
 
