@@ -290,7 +290,7 @@ int fmpnp_abi_version(void) { return FMPNP_ABI_VERSION; }
 const char *fmpnp_build_info(void) {
     return "fmpnp gfx950: lm_kernel(NT=512 wave-owned blocks, CH=64, NV=32, fp64 accumulation, bilinear cell memo), "
            "pack_kernel(Sobel+HWC3), gather_ref_kernel; speculative_gathers=" FMPNP_STR(FMPNP_SPEC)
-           "; steady_helpers=" FMPNP_STR(FMPNP_SS) "; source_digest=" FMPNP_SOURCE_DIGEST;
+           "; steady_helpers=" FMPNP_STR(FMPNP_SS) "; ratio_forms=" FMPNP_STR(FMPNP_RATIO_FORMS) "; source_digest=" FMPNP_SOURCE_DIGEST;
 }
 
 int fmpnp_device_check(int device) {

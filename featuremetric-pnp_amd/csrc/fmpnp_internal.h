@@ -23,6 +23,13 @@
 #define FMPNP_SS 0
 #endif
 
+// The ratio test's form chosen per evaluation from the previous evaluation's gather count
+// (FMPNP_RATIO_GTHR at run time): no threshold won both starts, so its
+// bookkeeping (an LDS atomic per gathering block) is compiled only into a -DFMPNP_RATIO_FORMS=1 build.
+#ifndef FMPNP_RATIO_FORMS
+#define FMPNP_RATIO_FORMS 0
+#endif
+
 namespace fmpnp {
 
 constexpr int NT = 512;         // threads per workgroup of the LM kernel (8 waves)

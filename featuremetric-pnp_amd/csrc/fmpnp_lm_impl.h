@@ -1741,7 +1741,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
 #endif
         ngath += __popcll(m);
         // (the ratio variants count the evaluation's gathers: the next evaluation's form)
-        if (R1 && defer && m && lane == 0)
+        if (FMPNP_RATIO_FORMS && R1 && defer && m && lane == 0)
             __hip_atomic_fetch_add(&st.gcnt[q.cur_ev & 1], (int)__popcll(m), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
         if (HELP && q.hfirst && m) {
@@ -2871,7 +2871,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
             // the ratio test's form for this evaluation: the guessed limit after an evaluation that
             // gathered at least a.ratio_gthr texels (its pass 1 has the slack to hide the early partials),
             // else the two passes -- both give the same partials bit for bit (ratio_guess_check)
-            if constexpr (kRatio1)
+            if constexpr (kRatio1 && FMPNP_RATIO_FORMS)
                 q.r1 = (k == 0 || a.ratio_gthr <= 0 || ufirst(st.gcnt[(k + 1) & 1]) >= a.ratio_gthr) ? 1 : 0;
             // project, gather, loss (+ partials)
             // (double-buffered gathers in both builds; speculation in the latency build only)
@@ -2898,7 +2898,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
             if (TEAM) team_arrive();
             else __syncthreads();
             // (every wave read the previous evaluation's count at this evaluation's start)
-            if (kRatio1 && tid == 0) st.gcnt[(k + 1) & 1] = 0;
+            if (FMPNP_RATIO_FORMS && kRatio1 && tid == 0) st.gcnt[(k + 1) & 1] = 0;
             if (r1) {
                 // (FMPNP_DBG bit 5: every block re-formed -- the two-pass partials, for A/B tests;
                 // bit 6: the re-formed blocks counted in texel_gathers' high word)

@@ -778,6 +778,162 @@ static hipError_t pack_f_window_tiles(const fmpnp_problem *probs_dev, const fmpn
     return hipSuccess;
 }
 
+// ---------------------------------------------------------------------------------------
+// Multi-row windowed f-only packs (round 5; FMPNP_PACK_F_ROWS=0 keeps the one-row hwc_win_kernel
+// above for A/B).  A workgroup takes one 64-channel x 64-column tile over HR_R consecutive rows.  Per row: the
+// channel rows (16 lanes x 16 B = one 256-byte run each) land in the LDS tile, and right after the
+// barrier the NEXT row's loads are issued into the same registers, so they are in flight while
+// the current row's texels (16 lanes x 16 B = 256 contiguous bytes of channels each) are stored;
+// the grid has HR_R times fewer workgroups.  Plane 0 of the tile's rows is read once (wave r: row r);
+// rows without a marked texel are skipped (the tile when none has one), only the 16-byte column quads
+// holding a marked texel are loaded and only marked texels stored.  End to end at r = 5 (bench
+// end_to_end, 2 x interleaved, profiles/r05_pack_rows_ab.txt): 34.5-35.1 k against 33.4 k queries/s,
+// hard start 37.6-39.0 k against 35.5 k.  (The full pack keeps the one-row tiles: the same multi-row
+// tiles cost the RobotCar leg's C = 1664 full packs 4-9 %.)
+constexpr int HR_NT = 256, HR_CT = 64, HR_XT = 64, HR_R = HR_NT / HR_XT;  // 4 rows: wave r reads row r's flags
+constexpr int HR_QPR = HR_XT / 4, HR_NL = HR_CT * HR_QPR / HR_NT;       // 16-B units per channel row; loads per lane
+
+template <typename Tin>
+__device__ __forceinline__ void hr_load(const Tin *__restrict__ chw, int C, int H, int W, int c0, int x0, int y,
+                                        bool vec, const int *fl, float (&v)[HR_NL][4]) {
+    const int q = threadIdx.x % HR_QPR, x = x0 + 4 * q;
+    const bool quad = vec && x + 3 < W;
+    const bool want = fl[4 * q] | fl[4 * q + 1] | fl[4 * q + 2] | fl[4 * q + 3];
+#pragma unroll
+    for (int l = 0; l < HR_NL; ++l) {
+        const int c = c0 + (int)threadIdx.x / HR_QPR + l * (HR_NT / HR_QPR);
+        v[l][0] = v[l][1] = v[l][2] = v[l][3] = 0.f;
+        if (c < C && want) {
+            const Tin *src = chw + ((size_t)c * H + y) * W + x;
+            if (quad) {
+                if constexpr (sizeof(Tin) == 4) {
+                    const nf4 w = kNtLoad ? __builtin_nontemporal_load(reinterpret_cast<const nf4 *>(src))
+                                          : *reinterpret_cast<const nf4 *>(src);
+                    v[l][0] = w.x; v[l][1] = w.y; v[l][2] = w.z; v[l][3] = w.w;
+                } else {
+                    const double2 w0 = *reinterpret_cast<const double2 *>(src);
+                    const double2 w1 = *reinterpret_cast<const double2 *>(src + 2);
+                    v[l][0] = (float)w0.x; v[l][1] = (float)w0.y; v[l][2] = (float)w1.x; v[l][3] = (float)w1.y;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (x + k < W) v[l][k] = (float)src[k];
+            }
+        }
+    }
+}
+
+template <typename Tin>
+__device__ __forceinline__ void hr_tile(const Tin *__restrict__ chw, int C, int H, int W, float *__restrict__ out,
+                                        int cs, const unsigned char *__restrict__ win, int nct, int nxt, int vec_ok,
+                                        int b) {
+    constexpr int LD = HR_XT + 1;
+    __shared__ float tile[HR_CT * LD];
+    __shared__ int flag[HR_R][HR_XT];
+    __shared__ int rowany[HR_R];
+    const int ct = b % nct;
+    b /= nct;
+    const int xt = b % nxt, y0 = (b / nxt) * HR_R;
+    const int c0 = ct * HR_CT, x0 = xt * HR_XT;
+    const int rows = min(HR_R, H - y0);
+    const bool full_x = x0 + HR_XT <= W;
+    {
+        const int r = threadIdx.x / HR_XT, xx = threadIdx.x % HR_XT, x = x0 + xx;
+        const int f = r < rows && x < W && win[(size_t)(y0 + r) * W + x];
+        flag[r][xx] = f;
+        const bool any = __any(f);  // (HR_XT == 64: wave r holds row r)
+        if ((threadIdx.x & 63) == 0) rowany[r] = any;
+    }
+    __syncthreads();
+    int r = 0;
+    while (r < HR_R && !rowany[r]) ++r;
+    if (r == HR_R) return;  // no marked texel in the tile: nothing read, nothing written
+    float v[HR_NL][4];
+    hr_load<Tin>(chw, C, H, W, c0, x0, y0 + r, vec_ok && full_x, flag[r], v);
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    while (r < HR_R) {
+#pragma unroll
+        for (int l = 0; l < HR_NL; ++l) {
+            const int cc = (int)threadIdx.x / HR_QPR + l * (HR_NT / HR_QPR), q = threadIdx.x % HR_QPR;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) tile[cc * LD + 4 * q + k] = v[l][k];
+        }
+        __syncthreads();
+        int nr = r + 1;
+        while (nr < HR_R && !rowany[nr]) ++nr;
+        if (nr < HR_R) hr_load<Tin>(chw, C, H, W, c0, x0, y0 + nr, vec_ok && full_x, flag[nr], v);
+        constexpr int QPC = HR_CT / 4;
+        const int y = y0 + r;
+#pragma unroll
+        for (int l = 0; l < HR_XT * QPC / HR_NT; ++l) {
+            const int i = (int)threadIdx.x + l * HR_NT;
+            const int xx = i / QPC, cq = i - xx * QPC;
+            const int x = x0 + xx, c = c0 + 4 * cq;
+            if (flag[r][xx] && c < cs) {  // (flag: x < W and marked)
+                f4 o;
+                o.x = tile[(4 * cq + 0) * LD + xx];
+                o.y = tile[(4 * cq + 1) * LD + xx];
+                o.z = tile[(4 * cq + 2) * LD + xx];
+                o.w = tile[(4 * cq + 3) * LD + xx];
+                __builtin_nontemporal_store(o, reinterpret_cast<f4 *>(out + ((size_t)y * W + x) * cs + c));
+            }
+        }
+        __syncthreads();
+        r = nr;
+    }
+}
+
+template <typename Tin>
+__global__ __launch_bounds__(HR_NT) void hwc_rows_win_kernel(WinItems it) {
+    const int b = blockIdx.x;
+    int lo = 0, hi = it.n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (it.start[mid] <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    const fmpnp_problem &p = it.pd[lo];
+    hr_tile<Tin>(reinterpret_cast<const Tin *>(it.chw[lo]), p.c_end, p.Hf, p.Wf,
+                       reinterpret_cast<float *>(const_cast<void *>(p.feat)), p.cstride, p.window, it.nct[lo],
+                       it.nxt[lo], it.vec[lo], b - it.start[lo]);
+}
+
+static bool pack_f_rows() {
+    static const bool on = [] { const char *e = getenv("FMPNP_PACK_F_ROWS"); return !e || *e != '0'; }();
+    return on;
+}
+
+static hipError_t pack_f_window_rows(const fmpnp_problem *probs_dev, const fmpnp_problem *probs_host, int n,
+                                    const void *const *chw, int dtype_in, hipStream_t stream) {
+    const size_t es = dtype_in == FMPNP_F64 ? 8 : 4;
+    for (int i0 = 0; i0 < n; i0 += WB_MAX) {
+        WinItems it{};
+        const int m = std::min(n - i0, WB_MAX);
+        long total = 0;
+        for (int j = 0; j < m; ++j) {
+            const fmpnp_problem &p = probs_host[i0 + j];
+            if (p.cstride % 4 != 0 || ((uintptr_t)p.feat % 16) != 0 || !p.window) return hipErrorInvalidValue;
+            it.chw[j] = chw[i0 + j];
+            it.nct[j] = (p.cstride + HR_CT - 1) / HR_CT;
+            it.nxt[j] = (p.Wf + HR_XT - 1) / HR_XT;
+            it.vec[j] = ((uintptr_t)chw[i0 + j] % 16 == 0) && ((size_t)p.Wf * es) % 16 == 0;
+            it.start[j] = (int)total;
+            total += (long)it.nct[j] * it.nxt[j] * ((p.Hf + HR_R - 1) / HR_R);
+            if (total >= (1L << 31)) return hipErrorInvalidValue;
+        }
+        it.start[m] = (int)total;
+        it.n = m;
+        it.pd = probs_dev + i0;
+        if (total == 0) continue;
+        if (dtype_in == FMPNP_F32) hipLaunchKernelGGL(hwc_rows_win_kernel<float>, dim3((unsigned)total), dim3(HR_NT), 0, stream, it);
+        else hipLaunchKernelGGL(hwc_rows_win_kernel<double>, dim3((unsigned)total), dim3(HR_NT), 0, stream, it);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 hipError_t launch_pack_f_window(const fmpnp_problem *probs_dev, const fmpnp_problem *probs_host, int n,
                                 const void *const *chw, int dtype_in, int radius, int max_n, long max_hw,
                                 hipStream_t stream) {
@@ -797,6 +953,7 @@ hipError_t launch_pack_f_window(const fmpnp_problem *probs_dev, const fmpnp_prob
     // 4: 128 x 64, 5: 256 x 32, 6: 64 x 128.  End to end at radius 5 (tools/window_sweep.py, queries/s):
     // 64 x 64 33.1-33.2 k, 128 x 32 32.3-33.4 k, 64 x 32 30.7 k, 32 x 64 29.9 k, 256 x 32 26.5 k,
     // 128 x 64 25.5 k, 64 x 128 22.8 k (profiles/r04_window_tiles.txt)
+    if (pack_f_rows()) return pack_f_window_rows(probs_dev, probs_host, n, chw, dtype_in, stream);
     static const int tile = [] { const char *e = getenv("FMPNP_PACK_W_TILE"); return e ? atoi(e) : 1; }();
     switch (tile) {
     case 1: return pack_f_window_tiles<64, 64>(probs_dev, probs_host, n, chw, dtype_in, stream);

@@ -405,6 +405,8 @@ def test_ratio_form_choice_changes_nothing(B, init, ratio, monkeypatch):
     """The ratio variants choose per evaluation between the guessed limit and the two passes
     (FMPNP_RATIO_GTHR: the guess after an evaluation of at least that many texel gathers).  Both
     forms give the same partials, so any choice gives the same poses, costs, support and kept counts."""
+    if b"ratio_forms=1" not in _lib.load().fmpnp_build_info():
+        pytest.skip("per-evaluation ratio forms are compiled only into a -DFMPNP_RATIO_FORMS=1 build")
     probs = [packed_problem(synth.problem_inputs(512, 256, 240, 320, seed=40 + q, device=DEV, init=init))
              for q in range(B)]
     o = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, ratio_threshold=ratio, dtype=_lib.F32)
