@@ -37,10 +37,15 @@ def _initial_texels(X, K, R, t, W, H, Hf, Wf):
     return row, col
 
 
-@pytest.mark.parametrize("radius", [2, 5])
-def test_window_pack_writes_exactly_the_marked_texels(radius):
-    batches, (W, H) = synth.pipeline_queries(1, 3, N=200, C=37, Hf=30, Wf=44, device=DEV, seed0=70)
+# (Wf = 43: no 16-byte column quads, the per-texel loads and window reads; fp64 CHW input: the converting
+# loads; Hf = 30: a last tile of two rows; C = 37: a partial channel tile and a zero-padded stride)
+@pytest.mark.parametrize("radius,Wf_,dt", [(2, 44, "f32"), (5, 44, "f32"), (2, 43, "f32"), (5, 44, "f64"),
+                                           (5, 43, "f64")])
+def test_window_pack_writes_exactly_the_marked_texels(radius, Wf_, dt):
+    batches, (W, H) = synth.pipeline_queries(1, 3, N=200, C=37, Hf=30, Wf=Wf_, device=DEV, seed0=70)
     qs = batches[0]
+    if dt == "f64":
+        qs = [(a.double(), b, p, k) for (a, b, p, k) in qs]
     n = len(qs)
     C, Hf, Wf = qs[0][0].shape
     cs = (C + 3) // 4 * 4
@@ -62,7 +67,8 @@ def test_window_pack_writes_exactly_the_marked_texels(radius):
     d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(DEV)
     vp = ctypes.c_void_p
     rc = _lib.load().fmpnp_pack_features_f_window_batch(
-        vp(d_desc.data_ptr()), vp(desc.ctypes.data), n, (vp * n)(*[q[0].data_ptr() for q in qs]), _lib.F32, radius,
+        vp(d_desc.data_ptr()), vp(desc.ctypes.data), n, (vp * n)(*[q[0].data_ptr() for q in qs]),
+        _lib.F64 if dt == "f64" else _lib.F32, radius,
         _lib.stream_ptr(DEV))
     _lib.check(rc, "window pack")
     torch.cuda.synchronize()
