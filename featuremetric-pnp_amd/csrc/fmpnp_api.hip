@@ -194,7 +194,7 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     // CU busy there is no idle memory time to hide it in).  FMPNP_LM_WPS=2|4 forces a build.
     const char *wps_env = getenv("FMPNP_LM_WPS");
     const int want = wps_env ? atoi(wps_env) : 0;
-    const bool tp_ok = !bil_memo && opt->layout == FMPNP_LAYOUT_FGRAD && G == 1 && (long)n >= ncu &&
+    const bool tp_ok = !bil_memo && !windows && opt->layout == FMPNP_LAYOUT_FGRAD && G == 1 && (long)n >= ncu &&
                        2 * (lds_fixed_bytes() + (int)lm_dyn_lds_bytes(P.mmax, P.nc_max, false, bil_memo)) <= lds_cu;
     const bool tp = tp_ok && (want == WPS_THROUGHPUT || (want == 0 && (long)n >= 2L * ncu));
     P.wps = tp ? WPS_THROUGHPUT : WPS_LATENCY;
@@ -262,6 +262,8 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     P.var = P.spec ? spec_variant(lm_variant(*opt)) : lm_variant(*opt);
     if (P.ss) P.var = ss_variant(P.var);  // (the SS variants carry the first-evaluation hand-off too)
     else if (P.helpers) P.var = help_variant(P.var);
+    // (packed windows: the variant with the window check; the f-only variants always carry theirs)
+    if (windows && opt->layout == FMPNP_LAYOUT_FGRAD) P.var = win_variant(P.var);
     P.ratio = opt->use_ratio != 0;
     P.dtype = opt->dtype;
     *pl = P;

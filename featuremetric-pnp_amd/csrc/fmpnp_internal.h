@@ -150,6 +150,15 @@ inline int help_variant(int var) {
     return var == VAR_GM_SPEC ? VAR_GM_SPEC_H : var == VAR_NEAREST_SPEC ? VAR_NEAREST_SPEC_H
          : var == VAR_GM ? VAR_GM_H : var == VAR_NEAREST ? VAR_NEAREST_H : var;
 }
+// ... and the packed non-speculating ones with the packed-window check compiled in (a window on the
+// f, gx, gy planes: fmpnp_feature_pnp's windowed packs); without a window the check's code alone cost
+// the non-speculating variants up to 6 %, so the other variants do not carry it
+constexpr int VAR_GM_W = FMPNP_VAR_GM_W, VAR_NEAREST_W = FMPNP_VAR_NEAREST_W, VAR_GM_H_W = FMPNP_VAR_GM_H_W,
+              VAR_NEAREST_H_W = FMPNP_VAR_NEAREST_H_W;
+inline int win_variant(int var) {
+    return var == VAR_GM ? VAR_GM_W : var == VAR_NEAREST ? VAR_NEAREST_W : var == VAR_GM_H ? VAR_GM_H_W
+         : var == VAR_NEAREST_H ? VAR_NEAREST_H_W : var;
+}
 int lm_variant(const fmpnp_options &o);
 const void *lm_kernel_ptr(int dtype, int wps, bool team, bool ratio, int var);
 

@@ -35,6 +35,20 @@ static LmFn pick_var(int var) {
         }
         return nullptr;
     }
+    if (var == VAR_GM_W || var == VAR_NEAREST_W) {  // packed windows (fmpnp_feature_pnp): latency build
+        if constexpr (WPS == WPS_LATENCY) {
+            if (var == VAR_GM_W) return lm_kernel<float, WPS, TEAM, RATIO, VAR_GM_W>;
+            return lm_kernel<float, WPS, TEAM, RATIO, VAR_NEAREST_W>;
+        }
+        return nullptr;
+    }
+    if (var == VAR_GM_H_W || var == VAR_NEAREST_H_W) {  // ... with the first-evaluation helpers
+        if constexpr (WPS == WPS_LATENCY && !TEAM) {
+            if (var == VAR_GM_H_W) return lm_kernel<float, WPS, TEAM, RATIO, VAR_GM_H_W>;
+            return lm_kernel<float, WPS, TEAM, RATIO, VAR_NEAREST_H_W>;
+        }
+        return nullptr;
+    }
     if (var == VAR_BILINEAR) return nullptr;  // the cell memo runs on the WPS_WIDE build only
     if (var == VAR_BIL_DIRECT) return lm_kernel<float, WPS, TEAM, RATIO, VAR_BIL_DIRECT>;
     if constexpr (WPS == WPS_LATENCY) {  // FMPNP_LAYOUT_F (the planner keeps it on the latency build)

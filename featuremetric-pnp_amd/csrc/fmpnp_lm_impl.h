@@ -1605,7 +1605,8 @@ __device__ __forceinline__ void spec_pass(const PC &q, int mmax, long long &ngat
 // HS: the steady-state helpers fill the idle slots (ss_fill): every wave keeps two slots, none predicts.
 // R1: the ratio test with a guessed limit (ratio_guess_check): the block partials are formed in
 // this pass with the previous evaluation's limit, and each block's |rho| statistics are parked.
-template <typename T, bool PIPE, bool FL, bool SP, bool HELP, bool HS = false, bool R1 = false>
+// WN: the packed-window check (the _W variants: a window on the packed f, gx, gy planes).
+template <typename T, bool PIPE, bool FL, bool SP, bool HELP, bool HS = false, bool R1 = false, bool WN = false>
 __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ngath, const double pose[12]) {
     LMState &st = S();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1713,27 +1714,36 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
             }
         }
         unsigned long long m = __ballot(dirty);
-        // (not in the speculating variants: the planner never gives them a window, and the check costs
-        // the headline 1 % -- profiles/r05_window_check_ab.txt)
-        if constexpr (FL || !SP) {
-            // packed window (fmpnp_pack_features_f_window_batch; fmpnp_feature_pnp's windowed packs):
-            // every texel gathered must be packed -- for the f-only layout its whole 3x3 neighbourhood
-            // (plane 1, st.c.win_ok), for the packed f, gx, gy planes the texel itself (plane 0, Hf * Wf
-            // bytes before).  A miss is never read; it marks the problem's result invalid
-            // (FMPNP_STATUS_WINDOW: the caller packs in full and refines again).  The f-only layout stops
-            // the problem after this evaluation (abort_flag, read only after barriers: one workgroup per
-            // problem); the packed layout finishes it (a team's members never wait on a stopped one)
+        // packed windows (fmpnp_pack_features_f_window_batch; fmpnp_feature_pnp's windowed packs): every
+        // texel gathered must be packed.  A miss marks the problem's result invalid (FMPNP_STATUS_WINDOW:
+        // the caller packs in full and refines again).
+        if constexpr (FL) {
+            // the f-only layout: the texel's whole 3x3 neighbourhood (plane 1, st.c.win_ok); a miss is
+            // never read and stops the problem after this evaluation (abort_flag, read only after
+            // barriers: one workgroup per problem)
             const unsigned char *wok = ufirst(st.c.win_ok);
             if (wok != nullptr && m) {
-                const bool miss = ((m >> lane) & 1ull) && wok[FL ? off : off - q.Hf * q.Wf] == 0;
+                const bool miss = ((m >> lane) & 1ull) && wok[off] == 0;
                 const unsigned long long mm = __ballot(miss);
                 if (mm) {
                     m &= ~mm;  // (never read an unpacked texel)
                     if (lane == 0) {
                         st.win_miss = 1;
-                        if (FL) st.abort_flag = 1;
+                        st.abort_flag = 1;
                     }
                 }
+            }
+        } else if constexpr (WN) {
+            // the packed f, gx, gy planes: the texel itself (plane 0, Hf * Wf bytes before plane 1).  A
+            // miss is only flagged: the texel is read as usual (inside the full-size map, its bytes
+            // stale) and the problem finishes, so a team's members never wait on a stopped one.  Only the
+            // _W variants carry the check: compiled into the plain non-speculating variants it cost them up
+            // to 6 % with no window at all (profiles/r05_window_check_fgrad_ab.txt), and 1 % of the
+            // headline in the speculating ones (profiles/r05_window_check_ab.txt)
+            const unsigned char *wok = ufirst(st.c.win_ok);
+            if (wok != nullptr && m) {
+                const bool miss = ((m >> lane) & 1ull) && wok[off - q.Hf * q.Wf] == 0;
+                if (__ballot(miss) && lane == 0) st.win_miss = 1;
             }
         }
 #if FMPNP_STAMPS
@@ -2800,7 +2810,10 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
 #endif
     constexpr bool kSS = WPS == WPS_LATENCY && !TEAM && (VAR == VAR_GM_SS || VAR == VAR_NEAREST_SS);
     constexpr bool kHelp = WPS == WPS_LATENCY && !TEAM && (VAR == VAR_GM_SPEC_H || VAR == VAR_NEAREST_SPEC_H ||
-                                                           VAR == VAR_GM_H || VAR == VAR_NEAREST_H || kSS);
+                                                           VAR == VAR_GM_H || VAR == VAR_NEAREST_H ||
+                                                           VAR == VAR_GM_H_W || VAR == VAR_NEAREST_H_W || kSS);
+    // the packed-window check (fmpnp_problem.window on the f, gx, gy planes)
+    constexpr bool kWin = VAR == VAR_GM_W || VAR == VAR_NEAREST_W || VAR == VAR_GM_H_W || VAR == VAR_NEAREST_H_W;
     if (helper) {
         if constexpr (kHelp) helper_run<T>(a, mmax);
         return;
@@ -2841,7 +2854,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
             r.spec = kSpec ? 1 : 0;
             if constexpr (kSpec) r.no_memo = 0;
             if constexpr (VAR == VAR_GM || VAR == VAR_F_GM || VAR == VAR_GM_SPEC || VAR == VAR_GM_SPEC_H ||
-                          VAR == VAR_GM_H || VAR == VAR_GM_SS)
+                          VAR == VAR_GM_H || VAR == VAR_GM_SS || VAR == VAR_GM_W || VAR == VAR_GM_H_W)
                 r.loss = FMPNP_GEMAN_MCCLURE;
             r.bilinear = (VAR == VAR_BILINEAR || VAR == VAR_BIL_DIRECT) ? 1 : 0;
             return r;
@@ -2880,7 +2893,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
             if constexpr (VAR == VAR_BILINEAR)
                 lmax = eval_pass_bil<T>(q, mmax, ngath);
             else
-                lmax = eval_pass<T, true, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST), kSpec, kHelp, kSS, kRatio1>(
+                lmax = eval_pass<T, true, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST), kSpec, kHelp, kSS, kRatio1, kWin>(
                     q, mmax, ngath, pose);
             // the ratio test: with one workgroup per problem of at most 8 blocks, the guessed limit
             // (ratio_guess_check, after barrier 1); otherwise the two passes (exchange, contrib_pass)

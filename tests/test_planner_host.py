@@ -140,7 +140,8 @@ def test_windowed_problems_plan_one_workgroup(monkeypatch):
     """A packed window (fmpnp_problem.window) on the f-only layout forces one workgroup per problem
     (a window miss stops the problem inside its workgroup); on the packed f/gx/gy planes a miss is
     only flagged, so the plan keeps its workgroups but drops the speculative gathers (they would read
-    predicted texels outside the window); bilinear sampling refuses windows."""
+    predicted texels outside the window) and takes the variant with the window check (_W); bilinear
+    sampling refuses windows."""
     o = rf.make_options(**GM)
     o.layout = _lib.LAYOUT_F
     i = plan(1, o)
@@ -150,6 +151,12 @@ def test_windowed_problems_plan_one_workgroup(monkeypatch):
     i = plan(128, rf.make_options(**GM))
     assert i["speculate"] == 1 and i["variant_name"] == "GM_SPEC"
     i = plan(128, rf.make_options(**GM), window=True)
-    assert i["speculate"] == 0 and i["variant_name"] == "GM"
+    assert i["speculate"] == 0 and i["variant_name"] == "GM_W" and i["build_name"] == "latency"
+    i = plan(1, rf.make_options(**GM), window=True)  # (one problem: the first-evaluation helpers too)
+    assert i["variant_name"] in ("GM_W", "GM_H_W")
+    i = plan(512, rf.make_options(**GM), window=True)  # (no throughput build: it has no _W variant)
+    assert i["variant_name"] == "GM_W" and i["build_name"] == "latency"
+    i = plan(512, rf.make_options(**GM))
+    assert i["variant_name"] == "GM" and i["build_name"] == "throughput"
     with pytest.raises(_lib.FmpnpError):
         plan(1, rf.make_options(**dict(GM, sampling="bilinear")), window=True)
