@@ -1623,7 +1623,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
                      cb % V == 0 && (ce - cb) % V == 0;
     const bool defer = q.use_ratio != 0;
     // (the guessed-limit ratio test: one workgroup per problem of at most 8 blocks)
-    const bool r1 = R1 && defer && q.M <= 8 * 64 && q.r1;
+    const bool r1 = R1 && defer && q.M <= 8 * 64 && (!FMPNP_RATIO_FORMS || q.r1);
     const double rguess = r1 ? ufirst(st.rguess[q.cur_ev & 1]) : 0.0;
     // (a wave below spec_w0 keeps slot 0 and no predictions: the memoised path)
     // (HS with a.ss == 2, the prefetch-only helpers: the main speculates as the _SPEC variants do)
@@ -2897,13 +2897,13 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
                     q, mmax, ngath, pose);
             // the ratio test: with one workgroup per problem of at most 8 blocks, the guessed limit
             // (ratio_guess_check, after barrier 1); otherwise the two passes (exchange, contrib_pass)
-            const bool r1 = kRatio1 && q.use_ratio && q.M <= 8 * 64 && q.r1;
+            const bool r1 = kRatio1 && q.use_ratio && q.M <= 8 * 64 && (!FMPNP_RATIO_FORMS || q.r1);
             if (q.use_ratio && !r1) {
                 if (!ratio_exchange(lmax)) break;
                 const double limit = ufirst(st.rho_max) * st.c.ratio_thr;
                 contrib_pass(q, mmax, limit);
                 // (the next evaluation's guess, should it take the guessed form)
-                if (kRatio1 && tid == 0) st.rguess[(k + 1) & 1] = isnan(limit) ? INFINITY : limit;
+                if (FMPNP_RATIO_FORMS && kRatio1 && tid == 0) st.rguess[(k + 1) & 1] = isnan(limit) ? INFINITY : limit;
             }
             const int wave = tid >> 6;
             constexpr bool FLV = VAR == VAR_F_GM || VAR == VAR_F_NEAREST;
