@@ -26,6 +26,17 @@ pipe = RefinePipeline(img, storage=torch.float32, depth=2, window=int(os.environ
 pipe.run(batches)
 torch.cuda.synchronize()
 pr = cProfile.Profile()
+if os.environ.get("PREP_ONLY"):  # one batch's host preparation, 10 times (cumulative time per callee)
+    import time
+    t0 = time.perf_counter()
+    pr.enable()
+    for _ in range(10):
+        pipe._prepare(list(batches[0]), 0)
+    pr.disable()
+    torch.cuda.synchronize()
+    print(f"_prepare: {(time.perf_counter() - t0) / 10 * 1e3:.3f} ms per batch of {B} (profiled)")
+    pstats.Stats(pr).sort_stats("cumulative").print_stats(40)
+    sys.exit(0)
 pr.enable()
 pipe.run(batches)
 torch.cuda.synchronize()
