@@ -52,6 +52,17 @@ class sparseFeaturePnP(nn.Module):
         self.status_ = None
         self.last_result_ = None
 
+    def __setattr__(self, name, value):
+        # plain attributes (iterations, loss_fn, the status and result fields) skip nn.Module's
+        # parameter / buffer / submodule bookkeeping: a model is built per query by the consumer
+        # (gin, optimize_feature_pnp.py:63), so its construction is part of every call's latency.
+        # Tensors (initial_cost_, best_cost_) and modules keep nn.Module's path.
+        if isinstance(value, (torch.Tensor, nn.Module)) or name in self.__dict__.get("_parameters", ()) \
+                or name in self.__dict__.get("_buffers", ()) or name in self.__dict__.get("_modules", ()):
+            nn.Module.__setattr__(self, name, value)
+        else:
+            object.__setattr__(self, name, value)
+
     # -- reference API --------------------------------------------------------
     def track(self, R, t, cost, points_2d, mask, threshold_mask):
         self.track_["Rs"].append(R)
