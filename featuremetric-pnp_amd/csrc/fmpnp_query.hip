@@ -192,6 +192,12 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
         hd[r].fref = d_fref;
         hd[r].pts3d = d_pts;
     }
+    // an error once work is queued: wait for the stream before returning, so the pinned staging buffer
+    // and the device carve are never reused (by the next call) while an earlier copy still reads them
+    auto drain = [s](int code) {
+        (void)hipStreamSynchronize(s);
+        return code;
+    };
   for (int attempt = 0; attempt < 2; ++attempt) {
     // attempt 0: windowed when asked; attempt 1 (only after a window miss): the full pack
     const bool win = attempt == 0 && window_radius > 0;
@@ -204,41 +210,41 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
     }
     memcpy(h + b_inl + b_pts, hd, sizeof(fmpnp_problem) * n_res);
     e = hipMemcpyAsync(d, h, up, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return (int)e;
+    if (e != hipSuccess) return drain((int)e);
     e = hipMemsetAsync(d_err, 0, sizeof(int), s);
-    if (e != hipSuccess) return (int)e;
+    if (e != hipSuccess) return drain((int)e);
     if (trace) {
         e = hipMemsetAsync(d_tr, 0, b_tr, s);
-        if (e != hipSuccess) return (int)e;
+        if (e != hipSuccess) return drain((int)e);
     }
     // pack (optimize_feature_pnp.py:57,61): the Sobel pack writes channels < C, so a padded
     // stride is zeroed first; the f-only copy fills the padding itself
     if (!lay_f && cs != C) {
         e = hipMemsetAsync(d_feat, 0, b_feat, s);
-        if (e != hipSuccess) return (int)e;
+        if (e != hipSuccess) return drain((int)e);
     }
     if (win) {
         // only the texels within window_radius of a point's texel at (R0, t0) (its square in plane 0 of
         // the window map): the refinement reads the texels its points visit, a few from where they
         // start; the LM flags a gather outside the window (FMPNP_STATUS_WINDOW) and the call re-runs
         e = launch_win_mark(d_desc, 1, window_radius, N, (long)H * W, s);
-        if (e != hipSuccess) return (int)e;
+        if (e != hipSuccess) return drain((int)e);
         e = launch_pack_win(query_chw, dtype_query, C, H, W, d_feat, opt->dtype, cs, opt->sobel_flags & 1,
                             (opt->sobel_flags >> 1) & 1, d_win, s);
     } else {
         e = launch_pack(query_chw, nullptr, nullptr, dtype_query, C, H, W, d_feat, opt->dtype, cs,
                         opt->sobel_flags & 1, (opt->sobel_flags >> 1) & 1, s, planes);
     }
-    if (e != hipSuccess) return (int)e;
+    if (e != hipSuccess) return drain((int)e);
     // fref (optimize_feature_pnp.py:51-56): the reference map's first C channels
     if (N > 0) {
         if (cs != C) {
             e = hipMemsetAsync(d_fref, 0, b_fref, s);
-            if (e != hipSuccess) return (int)e;
+            if (e != hipSuccess) return drain((int)e);
         }
         e = launch_gather_ref(ref_chw, dtype_ref, C_ref, H_ref, W_ref, d_inl, N, img0, img1, d_fref, opt->dtype, cs,
                               d_err, s);
-        if (e != hipSuccess) return (int)e;
+        if (e != hipSuccess) return drain((int)e);
     }
     // the LM launches
     for (int r = 0; r < n_res; ++r) {
@@ -248,7 +254,7 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
             // fixed-order reduction -- one evaluation, so not an LM launch (a latency chain there)
             e = launch_compute_cost(hd[0], opt->layout, opt->dtype, opt->use_ratio, opt->ratio_threshold, d_cost, d_sup,
                                     d_res, s);
-            if (e != hipSuccess) return (int)e;
+            if (e != hipSuccess) return drain((int)e);
             continue;
         }
         if (n_levels > 0 && r >= 2) {
@@ -258,17 +264,17 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
             e = hipMemcpyAsync((unsigned char *)(d_desc + r) + offsetof(fmpnp_problem, R0),
                                (const unsigned char *)(d_res + r - 1) + offsetof(fmpnp_result, R), 96,
                                hipMemcpyDeviceToDevice, s);
-            if (e != hipSuccess) return (int)e;
+            if (e != hipSuccess) return drain((int)e);
         }
         fmpnp_trace_entry *tr = (trace && !cost) ? d_tr + (size_t)(n_levels > 0 ? r - 1 : 0) * stride : nullptr;
         rc = fmpnp_refine_batch_async(d_desc + r, &hd[r], 1, N, opt, d_res + r, tr, stride, d_ws, ws, hip_stream);
-        if (rc) return rc;
+        if (rc) return drain(rc);
     }
     // the one download
     e = hipMemcpyAsync(h, d_res, down, hipMemcpyDeviceToHost, s);
-    if (e != hipSuccess) return (int)e;
+    if (e != hipSuccess) return drain((int)e);
     e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return (int)e;
+    if (e != hipSuccess) return drain((int)e);
     bool miss = false;
     for (int r = 0; r < n_res; ++r) miss = miss || (((const fmpnp_result *)h)[r].status & FMPNP_STATUS_WINDOW);
     if (win && miss) {
