@@ -3,37 +3,8 @@
 // One launch runs the WHOLE Levenberg-Marquardt loop of every problem of a batch
 // (sparseFeaturePnP.forward, featurePnP/model.py:245-494) on the device.
 //
-// Work decomposition
-//   * A "team" of G workgroups (512 threads = 8 waves each) owns one problem at a time;
-//     teams walk the batch persistently (problem = team, team + T, ...).
-//   * Points are cut into chunks of CH = 16; workgroup s of a team owns a contiguous
-//     range of chunks, and wave w of the workgroup owns the 64-point blocks w, w+8, ...
-//     of that range.  Per evaluation a wave carries each of its blocks from projection
-//     to chunk partials with NO workgroup barrier:
-//       project  (lane per point, fp64, exact pixel rounding) -> texel offset, P;
-//       gather   the points whose texel changed (ballot), two per wave: each half-wave
-//                issues 16-byte loads of the channels-last [H][W][3][C] texel and fref
-//                and reduces the six channel sums  sum e^2, sum gx e, sum gy e, sum gx^2,
-//                sum gx gy, sum gy^2  in fp64 (the C x 6 Jacobian is never materialised:
-//                J = G A with the 2x6 pose chain A, so J^T e = A^T (G^T e),
-//                J^T J = A^T (G^T G) A); unchanged texels keep their sums (memoisation);
-//       loss + normal equations (lane per point) -> 21 + 6 entries, rho and counters,
-//                reduced per 16-point chunk by a fixed transposed DPP tree.
-//   * The chunk partials are summed by wave 0 with a fixed tree over CHUNK INDICES.  Results
-//     are therefore deterministic and independent of G: the LM accept test `new > prev`
-//     (model.py:469-472) compares costs that tie exactly whenever the pixel sets are
-//     equal, and a scheduling-dependent sum would break those ties.
-//   * G > 1: chunk partials go to a per-team slot with write-through (sc1) stores,
-//     every storing wave drains, one lane bumps the team's arrival counter, one lane
-//     polls it (bounded spin), one agent-scope acquire; then wave 0 of every member
-//     reads all partials and runs the identical 6x6 solve + LM update (no second exchange).
-//   * One evaluation per iteration: the trial evaluation at (R', t') also produces that
-//     pose's normal equations.  On acceptance they are the next linearisation; on
-//     rejection the cached ones are reused -- bit-identical to the reference's
-//     recomputation at the unchanged pose (model.py:472-476).
-//   * The ratio test (model.py:324-336) needs max|rho| over the team before any point's
-//     weight is known: with it, loss values are parked in LDS, the maximum is exchanged,
-//     and a second pass over the blocks forms the normal equations.
+// The kernel template and its work decomposition: fmpnp_lm_impl.h.  This unit holds the
+// variant choice (lm_variant), the launch and the LDS sizing.
 #include <hip/hip_runtime.h>
 
 #include "fmpnp.h"

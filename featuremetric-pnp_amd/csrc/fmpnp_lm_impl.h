@@ -1,18 +1,17 @@
 // fmpnp_lm_impl.h -- the LM kernel template (included by the per-storage-type
 // instantiation units fmpnp_lm_f32.hip / fmpnp_lm_f64.hip).
 #pragma once
-// fmpnp_lm.hip -- the feature-metric LM refiner on gfx950 (MI355X).
-//
-// One launch runs the WHOLE Levenberg-Marquardt loop of every problem of a batch
-// (sparseFeaturePnP.forward, featurePnP/model.py:245-494) on the device.
+// The feature-metric LM refiner on gfx950 (MI355X): one launch runs the WHOLE
+// Levenberg-Marquardt loop of every problem of a batch (sparseFeaturePnP.forward,
+// featurePnP/model.py:245-494) on the device.
 //
 // Work decomposition
 //   * A "team" of G workgroups (512 threads = 8 waves each) owns one problem at a time;
 //     teams walk the batch persistently (problem = team, team + T, ...).
-//   * Points are cut into chunks of CH = 16; workgroup s of a team owns a contiguous
-//     range of chunks, and wave w of the workgroup owns the 64-point blocks w, w+8, ...
-//     of that range.  Per evaluation a wave carries each of its blocks from projection
-//     to chunk partials with NO workgroup barrier:
+//   * Points are cut into chunks of CH = 64, one wave block each; workgroup s of a team owns a
+//     contiguous range of chunks, and wave w of the workgroup owns the blocks w, w+8, ... of that
+//     range.  Per evaluation a wave carries each of its blocks from projection to its chunk
+//     partial with NO workgroup barrier:
 //       project  (lane per point, fp64, exact pixel rounding) -> texel offset, P;
 //       gather   the points whose texel changed (ballot), two per wave: each half-wave
 //                issues 16-byte loads of the channels-last [H][W][3][C] texel and fref
@@ -21,7 +20,7 @@
 //                J = G A with the 2x6 pose chain A, so J^T e = A^T (G^T e),
 //                J^T J = A^T (G^T G) A); unchanged texels keep their sums (memoisation);
 //       loss + normal equations (lane per point) -> 21 + 6 entries, rho and counters,
-//                reduced per 16-point chunk by a fixed transposed DPP tree.
+//                reduced per 64-point chunk by a fixed transposed permlane/DPP tree.
 //   * The chunk partials are summed by wave 0 with a fixed tree over CHUNK INDICES.  Results
 //     are therefore deterministic and independent of G: the LM accept test `new > prev`
 //     (model.py:469-472) compares costs that tie exactly whenever the pixel sets are
@@ -34,9 +33,11 @@
 //     pose's normal equations.  On acceptance they are the next linearisation; on
 //     rejection the cached ones are reused -- bit-identical to the reference's
 //     recomputation at the unchanged pose (model.py:472-476).
-//   * The ratio test (model.py:324-336) needs max|rho| over the team before any point's
-//     weight is known: with it, loss values are parked in LDS, the maximum is exchanged,
-//     and a second pass over the blocks forms the normal equations.
+//   * The ratio test (model.py:324-336) needs max|rho| over the problem before any point's
+//     weight is known.  One workgroup per problem of at most 8 blocks: the partials are formed
+//     with the previous evaluation's limit and a block whose kept set the true limit changes is
+//     re-formed (ratio_guess_check); otherwise loss values are parked in LDS, the maximum is
+//     exchanged, and a second pass over the blocks forms the normal equations (contrib_pass).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stddef.h>
