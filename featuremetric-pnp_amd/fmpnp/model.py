@@ -36,21 +36,17 @@ class sparseFeaturePnP(nn.Module):
     def __init__(self, n_iters, loss_fn=_losses.squared_loss, lambda_=0.01, verbose=False, ratio_threshold=None,
                  useGPU=False, storage=None, device=None, wgs_per_problem=0, sampling="nearest"):
         super().__init__()
-        self.iterations = n_iters
-        self.loss_fn = loss_fn
-        self.verbose = verbose
-        self.lambda_ = lambda_
-        self.track_ = {"Rs": [], "ts": [], "costs": [], "points2d": [], "mask": [], "threshold_mask": []}
-        self.use_ratio_test_ = ratio_threshold is not None
-        self.ratio_threshold_ = ratio_threshold
-        self.initial_cost_ = None
-        self.useGPU = useGPU  # accepted for compatibility: the refiner always runs on the GPU
-        self.storage = storage
-        self.device = device
-        self.wgs_per_problem = wgs_per_problem
-        self.sampling = sampling  # extension: "bilinear" samples 2x2 taps (the reference: "nearest")
-        self.status_ = None
-        self.last_result_ = None
+        self.loss_fn = loss_fn  # (a module-valued loss keeps nn.Module's registration)
+        # the plain attributes in one update (none is a tensor or a module: __setattr__ would
+        # route each to object.__setattr__ anyway)
+        self.__dict__.update(
+            iterations=n_iters, verbose=verbose, lambda_=lambda_,
+            track_={"Rs": [], "ts": [], "costs": [], "points2d": [], "mask": [], "threshold_mask": []},
+            use_ratio_test_=ratio_threshold is not None, ratio_threshold_=ratio_threshold, initial_cost_=None,
+            useGPU=useGPU,  # accepted for compatibility: the refiner always runs on the GPU
+            storage=storage, device=device, wgs_per_problem=wgs_per_problem,
+            sampling=sampling,  # extension: "bilinear" samples 2x2 taps (the reference: "nearest")
+            status_=None, last_result_=None)
 
     def __setattr__(self, name, value):
         # plain attributes (iterations, loss_fn, the status and result fields) skip nn.Module's

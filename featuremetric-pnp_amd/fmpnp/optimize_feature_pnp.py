@@ -7,12 +7,13 @@ LM loop on the CPU (optimize_feature_pnp.py:51-69).  Here the query hypercolumn
 stays on the device: one fused Sobel + channels-last pack kernel, one gather
 kernel for the reference descriptors, one LM launch.
 """
+import ctypes
 import os
 
 import numpy as np
 import torch
 
-from . import config
+from . import _lib, config
 from . import refine as _rf
 from .matrix_utils import matrix_quaternion
 from .model import _find_inliers_packed, sparseFeaturePnP
@@ -136,10 +137,11 @@ def window_radius(C, H, W, N):
     return 6 if C > 256 else 0
 
 
+_DP = ctypes.POINTER(ctypes.c_double)
+
+
 def _feature_pnp_one_call(model, q, r, prediction, K, image_shape, track, levels, storage, layout, window=None):
     """feature_pnp through fmpnp_feature_pnp: one host call, one host wait (optimize_feature_pnp.py:50-71)."""
-    import ctypes
-    from . import _lib
     r = r[0] if r.dim() == 4 else r
     q, r = q.contiguous(), r.contiguous()
     dev = q.device
@@ -160,20 +162,21 @@ def _feature_pnp_one_call(model, q, r, prediction, K, image_shape, track, levels
         window = window_radius(C, H, W, pts.shape[0])
     if layout != "fgrad" or getattr(model, "sampling", "nearest") != "nearest":
         window = 0
-    lv = (_lib.Level * max(n_lv, 1))(*[_lib.Level(a, b) for a, b in (levels or [])])
+    lv = (_lib.Level * n_lv)(*[_lib.Level(a, b) for a, b in levels]) if n_lv else None
     res = np.zeros(n_lv + 1 if n_lv else 1, dtype=_rf.RESULT_DTYPE)
     want_trace = bool(track) or bool(model.verbose)
     stride = model.iterations + 1
     tr = (_lib.TraceEntry * (max(n_lv, 1) * stride))() if want_trace else None
-    dp = ctypes.POINTER(ctypes.c_double)
-    vp = ctypes.c_void_p
-    with torch.cuda.device(dev):
-        rc = _lib.load().fmpnp_feature_pnp(
-            vp(q.data_ptr()), _rf._dtype_code(q.dtype), C, H, W, vp(r.data_ptr()), _rf._dtype_code(r.dtype),
-            r.shape[0], r.shape[1], r.shape[2], vp(inl.ctypes.data), vp(pts.ctypes.data), pts.shape[0],
-            Kn.ctypes.data_as(dp), R0.ctypes.data_as(dp), t0.ctypes.data_as(dp), int(image_shape[0]),
-            int(image_shape[1]), lv if n_lv else None, n_lv, ctypes.byref(opts), int(window), vp(res.ctypes.data), tr,
-            stride if want_trace else 0, _lib.stream_ptr(dev))
+    # (c_void_p arguments take plain addresses; the device switch only when the map is not on the current one)
+    args = (q.data_ptr(), _rf._dtype_code(q.dtype), C, H, W, r.data_ptr(), _rf._dtype_code(r.dtype), r.shape[0],
+            r.shape[1], r.shape[2], inl.ctypes.data, pts.ctypes.data, pts.shape[0], Kn.ctypes.data_as(_DP),
+            R0.ctypes.data_as(_DP), t0.ctypes.data_as(_DP), int(image_shape[0]), int(image_shape[1]), lv, n_lv,
+            ctypes.byref(opts), int(window), res.ctypes.data, tr, stride if want_trace else 0)
+    if dev.index == torch.cuda.current_device():
+        rc = _lib.load().fmpnp_feature_pnp(*args, _lib.stream_ptr(dev))
+    else:
+        with torch.cuda.device(dev):
+            rc = _lib.load().fmpnp_feature_pnp(*args, _lib.stream_ptr(dev))
     if rc == _lib.ERANGE:
         raise IndexError("a reference inlier maps outside the reference hypercolumn "
                          "(optimize_feature_pnp.py:56 raises IndexError)")
