@@ -188,7 +188,7 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     P.G = G;
     P.mmax = ((P.nc_max + G - 1) / G) * CH;
     P.lds = lds_for(G);
-    // build: with at least two problems per CU the throughput build (256-thread workgroups,
+    // build: with more problems than CUs the throughput build (256-thread workgroups,
     // two per CU: one problem's LM tail overlaps the other's point work) -- one workgroup per
     // problem, no speculation (its LDS would not leave room for two workgroups, and with every
     // CU busy there is no idle memory time to hide it in).  FMPNP_LM_WPS=2|4 forces a build.
@@ -196,7 +196,10 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     const int want = wps_env ? atoi(wps_env) : 0;
     const bool tp_ok = !bil_memo && !windows && opt->layout == FMPNP_LAYOUT_FGRAD && G == 1 && (long)n >= ncu &&
                        2 * (lds_fixed_bytes() + (int)lm_dyn_lds_bytes(P.mmax, P.nc_max, false, bil_memo)) <= lds_cu;
-    const bool tp = tp_ok && (want == WPS_THROUGHPUT || (want == 0 && (long)n >= 2L * ncu));
+    // (from more problems than CUs on: a second round of one-per-CU latency workgroups costs more than
+    // two throughput workgroups per CU -- ms per launch at B = 288 / 384 / 448 on 256 CUs: 0.684 / 0.700 /
+    // 0.721 latency against 0.580 / 0.606 / 0.632 throughput, profiles/r05_wps_mid_batch.txt)
+    const bool tp = tp_ok && (want == WPS_THROUGHPUT || (want == 0 && (long)n > ncu));
     P.wps = tp ? WPS_THROUGHPUT : WPS_LATENCY;
     if (bil_memo) P.wps = WPS_WIDE;  // the memo build's registers: one wave per SIMD
     if (tp || G > 1) {

@@ -86,6 +86,12 @@ def test_single_query_takes_helpers():
 def test_two_per_cu_takes_the_throughput_build():
     i = plan(1024, rf.make_options(**GM))
     assert (i["build_name"], i["variant_name"], i["wgs_per_problem"], i["speculate"]) == ("throughput", "GM", 1, 0)
+    # more problems than CUs (but fewer than two per CU): the throughput build too -- the latency build
+    # would run a second round of workgroups (profiles/r05_wps_mid_batch.txt); one per CU stays latency
+    i = plan(384, rf.make_options(**GM))
+    assert (i["build_name"], i["variant_name"]) == ("throughput", "GM")
+    i = plan(256, rf.make_options(**GM))
+    assert (i["build_name"], i["variant_name"]) == ("latency", "GM_SPEC")
 
 
 def test_ratio_and_variants():
