@@ -24,9 +24,9 @@ namespace {
 
 struct Plan {
     int G = 1, teams = 1, teams_pad = 8, gw = 8, grid = 8, nc_max = 1, max_n = 0;
-    int mmax = 0, lds = 0, wps = WPS_LATENCY, spec = 0, helpers = 0, grid_main = 8, ss = 0;
+    int mmax = 0, lds = 0, wps = WPS_LATENCY, spec = 0, helpers = 0, grid_main = 8;
     int var = 0, ratio = 0, dtype = 0;  // the kernel variant the launch runs
-    size_t ws_counters = 0, ws_partials = 0, ws_max = 0, ws_hrec = 0, ws_hflag = 0, ws_ss = 0, ws_total = 0;
+    size_t ws_counters = 0, ws_partials = 0, ws_max = 0, ws_hrec = 0, ws_hflag = 0, ws_total = 0;
 };
 
 thread_local Plan g_last;
@@ -238,15 +238,6 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
         const bool on = (!eh || atoi(eh) != 0) && opt->helpers >= 0;
         // (helpers beside the padded main grid, all resident at once: the mains wait on them)
         long spare = ((long)ncu - P.grid) / std::max(n, 1);
-        // the steady-state gather helpers (fmpnp_lm_impl.h ss_helper_run; opt-in, FMPNP_SS=1: records
-        // handed over, FMPNP_SS=2: prefetch only) take one spare CU per problem first.  Measured
-        // slower than the speculation alone at every cap, so off by default.
-        const char *es = getenv("FMPNP_SS");
-        const int ss = (FMPNP_SS && es) ? std::max(0, std::min(2, atoi(es))) : 0;
-        if (ss && opt->helpers >= 0 && P.spec && G == 1 && P.wps == WPS_LATENCY && P.teams == n && spare >= 1) {
-            P.ss = ss;
-            --spare;
-        }
         // (packed nearest memoised forward runs; a single helper per problem -- B > CUs/3 -- measured
         // slower at B = 128: 0.380 vs 0.360 ms, the first evaluation being HBM-bound there)
         if (on && G == 1 && P.wps == WPS_LATENCY && !bil_memo && opt->sampling == FMPNP_NEAREST &&
@@ -255,16 +246,12 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
             P.helpers = (int)std::min<long>(std::min<long>(std::min<long>(spare, P.nc_max), 8),
                                             opt->helpers > 0 ? opt->helpers : 8);
     }
-    P.grid = P.grid_main + n * P.helpers + (P.ss ? n : 0);
-    P.ws_ss = P.ss ? align_up((size_t)n * 24 * sizeof(double), 256) +
-                         align_up((size_t)n * P.nc_max * SS_BLK * sizeof(double), 256)
-                   : 0;
+    P.grid = P.grid_main + n * P.helpers;
     P.ws_hrec = P.helpers ? align_up((size_t)n * P.nc_max * CH * HREC * sizeof(double), 256) : 0;
     P.ws_hflag = P.helpers ? align_up((size_t)n * P.nc_max * sizeof(unsigned long long), 256) : 0;
-    P.ws_total = P.ws_counters + P.ws_partials + P.ws_max + P.ws_hrec + P.ws_hflag + P.ws_ss;
+    P.ws_total = P.ws_counters + P.ws_partials + P.ws_max + P.ws_hrec + P.ws_hflag;
     P.var = P.spec ? spec_variant(lm_variant(*opt)) : lm_variant(*opt);
-    if (P.ss) P.var = ss_variant(P.var);  // (the SS variants carry the first-evaluation hand-off too)
-    else if (P.helpers) P.var = help_variant(P.var);
+    if (P.helpers) P.var = help_variant(P.var);
     // (packed windows: the variant with the window check; the f-only variants always carry theirs)
     if (windows && opt->layout == FMPNP_LAYOUT_FGRAD) P.var = win_variant(P.var);
     P.ratio = opt->use_ratio != 0;
@@ -295,7 +282,7 @@ int fmpnp_abi_version(void) { return FMPNP_ABI_VERSION; }
 const char *fmpnp_build_info(void) {
     return "fmpnp gfx950: lm_kernel(NT=512 wave-owned blocks, CH=64, NV=32, fp64 accumulation, bilinear cell memo), "
            "pack_kernel(Sobel+HWC3), gather_ref_kernel; speculative_gathers=" FMPNP_STR(FMPNP_SPEC)
-           "; steady_helpers=" FMPNP_STR(FMPNP_SS) "; ratio_forms=" FMPNP_STR(FMPNP_RATIO_FORMS) "; source_digest=" FMPNP_SOURCE_DIGEST;
+           "; source_digest=" FMPNP_SOURCE_DIGEST;
 }
 
 int fmpnp_device_check(int device) {
@@ -480,21 +467,12 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
     a.grid_main = P.grid_main;
     a.hrec = (double *)(ws + P.ws_counters + P.ws_partials + P.ws_max);
     a.hflag = (unsigned long long *)(ws + P.ws_counters + P.ws_partials + P.ws_max + P.ws_hrec);
-    a.ss = P.ss;  // (1: records handed over; 2: the helpers only prefetch)
-    {
-        const char *e = getenv("FMPNP_SS_CAP");  // (measurement knob)
-        a.ss_cap = std::max(0, std::min(SS_CAP, e ? atoi(e) : 4));
-    }
-    a.ss_pose = P.ss ? (double *)(ws + P.ws_counters + P.ws_partials + P.ws_max + P.ws_hrec + P.ws_hflag) : nullptr;
-    a.ss_rec = P.ss ? a.ss_pose + align_up((size_t)n * 24 * sizeof(double), 256) / sizeof(double) : nullptr;
     {
         // flags from earlier launches carry smaller sequence numbers; the magic high bits keep
         // any other bytes the workspace held from matching
         static std::atomic<unsigned long long> seq{0};
         const unsigned long long sq = ++seq;
         a.htag = 0xF3A9000000000000ull | (sq & 0xFFFFFFFFFFFFull);
-        // the steady-state helpers' granule tag: the launch in bits 16..55 (the evaluation below)
-        a.sstag = 0x5A00000000000000ull | ((sq & 0xFFFFFFFFFFull) << 16);
     }
     a.mmax = P.mmax;
     a.stamps = g_stamps;
@@ -507,12 +485,6 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
         const char *ec = getenv("FMPNP_SPEC_CAP"), *ew = getenv("FMPNP_SPEC_W0");
         a.spec_cap = ec ? std::max(0, atoi(ec)) : 2;
         a.spec_w0 = ew ? std::max(0, atoi(ew)) : 3;  // round 3: wave 3 (no tail role) speculates too
-    }
-    {
-        // the ratio test's form per evaluation (measurement knob FMPNP_RATIO_GTHR; 0 = always the
-        // guessed limit)
-        const char *e = getenv("FMPNP_RATIO_GTHR");
-        a.ratio_gthr = e ? atoi(e) : 0;
     }
     {
         const char *e = getenv("FMPNP_DBG");  // debug knob, read per launch (fmpnp_internal.h LaunchArgs::dbg)

@@ -16,20 +16,6 @@
 #define FMPNP_SPEC 1
 #endif
 
-// Steady-state gather helpers (VAR_GM_SS / VAR_NEAREST_SS, opt-in FMPNP_SS=1|2 at run time): measured
-// slower than the speculation at every cap, so they are compiled only into a
-// -DFMPNP_SS=1 build (make EXTRA=-DFMPNP_SS=1) for repeating that measurement.
-#ifndef FMPNP_SS
-#define FMPNP_SS 0
-#endif
-
-// The ratio test's form chosen per evaluation from the previous evaluation's gather count
-// (FMPNP_RATIO_GTHR at run time): no threshold won both starts, so its
-// bookkeeping (an LDS atomic per gathering block) is compiled only into a -DFMPNP_RATIO_FORMS=1 build.
-#ifndef FMPNP_RATIO_FORMS
-#define FMPNP_RATIO_FORMS 0
-#endif
-
 namespace fmpnp {
 
 constexpr int NT = 512;         // threads per workgroup of the LM kernel (8 waves)
@@ -75,13 +61,6 @@ struct LaunchArgs {
     unsigned long long htag;      // this launch's flag value (a process-wide sequence + a magic)
     double *hrec;                 // [n][nc_max * CH][HREC] (six sums, then the texel offset)
     unsigned long long *hflag;    // [n][nc_max]
-    // steady-state gather helpers (VAR_*_SS): workgroups grid_main + n * helpers .. + n - 1, one per
-    // problem; ss_pose [n][24] and ss_rec [n][nc_max][SS_BLK] doubles of granules, sstag | (k + 1)
-    // the tag of evaluation k's granules (0xFFFF: the problem is done)
-    int ss, ss_cap;               // ss_cap <= SS_CAP: predictions gathered per block per evaluation
-    int ratio_gthr;               // ratio test: the guessed limit after >= this many gathers, else two passes
-    double *ss_pose, *ss_rec;
-    unsigned long long sstag;
 };
 constexpr int HREC = 7;
 
@@ -129,23 +108,6 @@ inline int spec_variant(int var) {
 // LaunchArgs::helpers; the headline-size batches run without it and without its code)
 constexpr int VAR_GM_SPEC_H = FMPNP_VAR_GM_SPEC_H, VAR_NEAREST_SPEC_H = FMPNP_VAR_NEAREST_SPEC_H,
               VAR_GM_H = FMPNP_VAR_GM_H, VAR_NEAREST_H = FMPNP_VAR_NEAREST_H;
-// ... and the steady-state gather helpers (fmpnp_lm_impl.h ss_helper_run / ss_fill): one more
-// workgroup per problem, on an idle CU, gathers the texels each point is predicted to move to at
-// the next evaluation and hands their six channel sums over; the main workgroup no longer predicts
-// or speculates itself (and compiles in the first-evaluation helpers' hand-off as well)
-constexpr int VAR_GM_SS = FMPNP_VAR_GM_SS, VAR_NEAREST_SS = FMPNP_VAR_NEAREST_SS;
-inline int ss_variant(int var) {
-    return (var == VAR_GM_SPEC || var == VAR_GM_SPEC_H) ? VAR_GM_SS
-         : (var == VAR_NEAREST_SPEC || var == VAR_NEAREST_SPEC_H) ? VAR_NEAREST_SS : var;
-}
-// steady-state helper hand-off, 16-byte granules {double value, u64 tag} (tag: the launch and
-// the evaluation; MI355X_MICROARCH.md "granule": one sc1 store each, no flag, no ordering):
-//   pose channel per problem: 12 granules (the pose of evaluation k, published by the main);
-//   records per problem and 64-point block: a count granule, then SS_CAP entries of 8 granules
-//   (point in the block, texel, the six channel sums)
-constexpr int SS_CAP = 16;
-constexpr int SS_ENT = 16;                   // doubles per entry (8 granules)
-constexpr int SS_BLK = (1 + SS_CAP) * SS_ENT; // doubles per block record
 inline int help_variant(int var) {
     return var == VAR_GM_SPEC ? VAR_GM_SPEC_H : var == VAR_NEAREST_SPEC ? VAR_NEAREST_SPEC_H
          : var == VAR_GM ? VAR_GM_H : var == VAR_NEAREST ? VAR_NEAREST_H : var;

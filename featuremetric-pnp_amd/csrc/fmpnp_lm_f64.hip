@@ -18,17 +18,6 @@ static LmFn pick_var(int var) {
         }
         return nullptr;
     }
-#if FMPNP_SS
-    if (var == VAR_GM_SS || var == VAR_NEAREST_SS) {  // steady-state gather helpers: latency build, G = 1
-        if constexpr (WPS == WPS_LATENCY && !TEAM) {
-            if (var == VAR_GM_SS) return lm_kernel<double, WPS, TEAM, RATIO, VAR_GM_SS>;
-            return lm_kernel<double, WPS, TEAM, RATIO, VAR_NEAREST_SS>;
-        }
-        return nullptr;
-    }
-#else
-    if (var == VAR_GM_SS || var == VAR_NEAREST_SS) return nullptr;  // (a -DFMPNP_SS=1 build only)
-#endif
     if (var == VAR_GM_H || var == VAR_NEAREST_H) {  // first-evaluation helpers without speculation
         if constexpr (WPS == WPS_LATENCY && !TEAM) {
             if (var == VAR_GM_H) return lm_kernel<double, WPS, TEAM, RATIO, VAR_GM_H>;

@@ -55,10 +55,6 @@ constexpr bool kSpecBuild = FMPNP_SPEC != 0;
 // its flags and pointers would otherwise hold scalar registers across the evaluation loop.
 // (FMPNP_STAMPS itself is defined in fmpnp_internal.h: it also sizes the LDS head)
 constexpr bool kStamps = FMPNP_STAMPS != 0;
-#ifndef FMPNP_TAIL_T2
-#define FMPNP_TAIL_T2 0  // 1: branch-free combine + 16-byte pose stores (measured +1.4 % at B = 128, -0.6 % at B = 1)
-#endif
-
 // dynamic LDS of the LM kernel (the only kernel in this file that uses LDS)
 extern __shared__ __attribute__((aligned(16))) unsigned char lm_lds[];
 
@@ -106,8 +102,6 @@ struct PC {
     int spec_cap;           // speculative gathers per wave per evaluation
     int spec_w0;            // the first wave that speculates
     int helpers;            // first-evaluation helper workgroups per problem (0: none)
-    int ss_fill;            // steady-state helpers hand records over (a.ss == 1; 2: they only prefetch)
-    int r1;                 // the ratio test of this evaluation takes the guessed limit (else the two passes)
     int hfirst;             // this is the problem's first evaluation
     int prob;               // the problem's index (helpers' record slots)
     const double *hrec;     // the helpers' records [n][nc_max * CH][HREC]
@@ -174,9 +168,6 @@ struct LMState {
     // rstat[b] = max|rho| of block b's supported points (NaN-propagating)
     double rguess[2];
     double rstat[8];
-    // texel gathers of evaluation k (ratio variants): gcnt[k & 1], the next evaluation's choice of
-    // ratio form (a.ratio_gthr)
-    int gcnt[2];
 #if FMPNP_STAMPS
     unsigned long long tlb[NT / 64][16];  // debug timeline (FMPNP_DBG bit 4), flushed at problem end
 #endif
@@ -242,6 +233,9 @@ __device__ __forceinline__ void dbg_stamp(bool on, int k) {
 #endif
 }
 __device__ __forceinline__ void tl_stamp(const PC &q, int k) {
+#if FMPNP_ISA_MARKS  // (ISA census build, tools/isa_census.py: a comment in the assembly at every stamp site)
+    asm volatile(";@@TL %0" ::"i"(k));
+#endif
 #if FMPNP_STAMPS
     if (q.tl && q.cur_eval == q.tl_eval && (threadIdx.x & 63) == 0)
         reinterpret_cast<LMState *>(lm_lds)->tlb[threadIdx.x >> 6][k] = __builtin_amdgcn_s_memtime();
@@ -490,7 +484,6 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
         st.abort_flag = 0;
         st.win_miss = 0;
         st.rguess[0] = st.rguess[1] = INFINITY;  // (evaluation 0: no guess -- every supported point kept)
-        st.gcnt[0] = st.gcnt[1] = 0;
         st.helper_absent = 0;
     }
     __syncthreads();
@@ -1603,11 +1596,10 @@ __device__ __forceinline__ void spec_pass(const PC &q, int mmax, long long &ngat
 // PIPE: double-buffered gathers (latency variant: the VGPRs for two pairs in flight).
 // SP: the variant can speculate (nearest sampling; bilinear never memoises).
 // ---------------------------------------------------------------------------
-// HS: the steady-state helpers fill the idle slots (ss_fill): every wave keeps two slots, none predicts.
 // R1: the ratio test with a guessed limit (ratio_guess_check): the block partials are formed in
 // this pass with the previous evaluation's limit, and each block's |rho| statistics are parked.
 // WN: the packed-window check (the _W variants: a window on the packed f, gx, gy planes).
-template <typename T, bool PIPE, bool FL, bool SP, bool HELP, bool HS = false, bool R1 = false, bool WN = false>
+template <typename T, bool PIPE, bool FL, bool SP, bool HELP, bool R1 = false, bool WN = false>
 __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ngath, const double pose[12]) {
     LMState &st = S();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1624,12 +1616,10 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
                      cb % V == 0 && (ce - cb) % V == 0;
     const bool defer = q.use_ratio != 0;
     // (the guessed-limit ratio test: one workgroup per problem of at most 8 blocks)
-    const bool r1 = R1 && defer && q.M <= 8 * 64 && (!FMPNP_RATIO_FORMS || q.r1);
+    const bool r1 = R1 && defer && q.M <= 8 * 64;
     const double rguess = r1 ? ufirst(st.rguess[q.cur_ev & 1]) : 0.0;
     // (a wave below spec_w0 keeps slot 0 and no predictions: the memoised path)
-    // (HS with a.ss == 2, the prefetch-only helpers: the main speculates as the _SPEC variants do)
-    const bool hs = HS && q.ss_fill;
-    const bool spec_on = SP && q.spec != 0 && (hs || wave >= q.spec_w0);
+    const bool spec_on = SP && q.spec != 0 && wave >= q.spec_w0;
     int *tex2 = lds_tex2(mmax, true), *spec = lds_spec(mmax, true), *slot = lds_slot(mmax, true);
     float *qp = lds_qp(mmax, true);
     double *rec2 = lds_rec2(mmax);
@@ -1663,11 +1653,9 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         if (SP) {  // (the speculating variants' arrays; unused below spec_w0)
             t2 = tex2[ii];
             sl = slot[ii];
-            if (!hs) {  // (with the steady-state helpers the idle slot's texel is tex2 itself)
-                qpx = qp[ii];
-                qpy = qp[mmax + ii];
-                sp = spec[ii];
-            }
+            qpx = qp[ii];
+            qpy = qp[mmax + ii];
+            sp = spec[ii];
         }
         const int old = valid ? old_r : -1;
         if (spec_on) {
@@ -1688,7 +1676,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
                 off = row * q.Wf + col;
                 if (FL) rc = (row << 16) | col;
                 if (q.bilinear) bilinear_taps(qx, qy, q.Hf, q.Wf, q.im_w, q.im_h, tp);
-                if (spec_on && !hs) {
+                if (spec_on) {
                     pred = spec_target(q, qx, qy, row, col, &qpx, &qpy);
                     qp[i] = qpx;
                     qp[mmax + i] = qpy;
@@ -1711,7 +1699,7 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
             if (spec_on) {
                 tex2[i] = moved ? old : t2;
                 if (moved) slot[i] = sl;
-                if (!hs) spec[i] = pred;
+                spec[i] = pred;
             }
         }
         unsigned long long m = __ballot(dirty);
@@ -1751,10 +1739,6 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
         if ((q.dbg & 128) && q.cur_ev > 0) m = 0;  // (diagnostics build, FMPNP_DBG bit 7: no gathers after eval 0 -- WRONG results, timing floor only)
 #endif
         ngath += __popcll(m);
-        // (the ratio variants count the evaluation's gathers: the next evaluation's form)
-        if (FMPNP_RATIO_FORMS && R1 && defer && m && lane == 0)
-            __hip_atomic_fetch_add(&st.gcnt[q.cur_ev & 1], (int)__popcll(m), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
         if (HELP && q.hfirst && m) {
             // first evaluation with helpers: the block's records at the initial pose come from a
             // helper workgroup (the same gather code at the same pose: identical sums); a point
@@ -2034,18 +2018,6 @@ __device__ __forceinline__ double combine_final_wave(int mmax, bool team, bool s
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
     const int NC = c.NC;
     double t = 0.0;
-#if FMPNP_TAIL_T2
-    if (!team && NC <= 8) {
-        // (one round: four unconditional loads -- a missing chunk reads chunk 0 and adds nothing)
-        const double *src = lds_part(mmax, spec);
-        double v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = src[(h + 2 * u < NC ? h + 2 * u : 0) * NV + j];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (h + 2 * u < NC) t += v[u];
-    } else
-#endif
     if (!team) {
         const double *src = lds_part(mmax, spec);
         double v[4];
@@ -2368,23 +2340,11 @@ __device__ __forceinline__ void lm_step_store(const double *hs, double delta[6],
 #pragma unroll
     for (int k = 0; k < 3; ++k) tc[k] = base[9 + k];
     pose_update(Rc, tc, delta, Rn, tn);
-#if FMPNP_TAIL_T2
-    double2 *o = reinterpret_cast<double2 *>(st.Ret[nxt]);  // (16-byte aligned: six 16-byte LDS writes)
-    if (lane == 0) {
-        o[0] = make_double2(Rn[0], Rn[1]);
-        o[1] = make_double2(Rn[2], Rn[3]);
-        o[2] = make_double2(Rn[4], Rn[5]);
-        o[3] = make_double2(Rn[6], Rn[7]);
-        o[4] = make_double2(Rn[8], tn[0]);
-        o[5] = make_double2(tn[1], tn[2]);
-    }
-#else
     double *o = st.Ret[nxt];
     if (lane == 0) {
         for (int k = 0; k < 9; ++k) o[k] = Rn[k];
         for (int k = 0; k < 3; ++k) o[9 + k] = tn[k];
     }
-#endif
 }
 
 __device__ __forceinline__ double clip_lam(double l) { return l < 1e-6 ? 1e-6 : (l > 1e4 ? 1e4 : l); }
@@ -2528,231 +2488,15 @@ __device__ __forceinline__ void helper_run(const LaunchArgs &a, int mmax) {
 }
 
 // ---------------------------------------------------------------------------
-// Steady-state gather helpers (VAR_*_SS).  With one workgroup per problem and an idle CU per
-// problem (B <= CUs / 2), a helper workgroup per problem takes over the speculative gathers:
-//   main, top of evaluation k:  its last wave publishes the pose of evaluation k (12 granules);
-//   helper:                     waits for it, projects every point at that pose, predicts each
-//                               point's texel at evaluation k + 1 (spec_target: the neighbour across
-//                               the near texel edge when the point moved farther than that edge's
-//                               distance), gathers the predicted texels with the main's own
-//                               gather_records (same code: bit-identical sums) and publishes, per
-//                               64-point block, up to SS_CAP entries {point, texel, six sums};
-//   main, after barrier 1:      the non-tail waves (ss_fill) read the block records tagged k and
-//                               put each entry's sums into its point's idle slot (tex2), where
-//                               evaluation k + 1 finds them if the point moves there.
-// Every granule carries the launch and evaluation tag and is one 16-byte sc1 store / load
-// (MI355X_MICROARCH.md: untorn, no ordering needed), so a record is used only if every granule is
-// evaluation k's; the main never waits for a helper (a late or absent helper costs on-demand
-// gathers, never a result), and a helper waits for the main's pose (bounded) or its "done".
-// The main workgroup no longer predicts or speculates: its VALU time goes to its own blocks.
-// ---------------------------------------------------------------------------
-typedef unsigned ss_u32x4 __attribute__((ext_vector_type(4)));
-constexpr int SS_DONE_K = 0xFFFE;  // ss_tag(SS_DONE_K): the main finished the problem
-__device__ __forceinline__ unsigned long long ss_tag(unsigned long long base, int k) {
-    return base | (unsigned long long)((k + 1) & 0xFFFF);
-}
-__device__ __forceinline__ void ss_put(__amdgpu_buffer_rsrc_t r, int voff, double v, unsigned long long tag) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    const ss_u32x4 d = {(unsigned)b, (unsigned)(b >> 32), (unsigned)tag, (unsigned)(tag >> 32)};
-    __builtin_amdgcn_raw_buffer_store_b128(d, r, voff, 0, 16);  // sc1: write-through
-}
-__device__ __forceinline__ ss_u32x4 ss_get(__amdgpu_buffer_rsrc_t r, int voff) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 16);  // sc1: from L2, never this CU's L1
-}
-__device__ __forceinline__ double ss_val(ss_u32x4 g) {
-    return __longlong_as_double((long long)(((unsigned long long)g.y << 32) | g.x));
-}
-__device__ __forceinline__ unsigned long long ss_tagof(ss_u32x4 g) { return ((unsigned long long)g.w << 32) | g.z; }
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t ss_pose_rsrc(const LaunchArgs &a, int p) {
-    return __builtin_amdgcn_make_buffer_rsrc(a.ss_pose + (size_t)p * 24, 0, 24 * 8, 0x00020000);
-}
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t ss_rec_rsrc(const LaunchArgs &a, int p) {
-    return __builtin_amdgcn_make_buffer_rsrc(a.ss_rec + (size_t)p * a.nc_max * SS_BLK, 0,
-                                             (int)((size_t)a.nc_max * SS_BLK * 8), 0x00020000);
-}
-// main: evaluation k's pose (Ret[k & 1]), or "done" (k = SS_DONE_K), lanes 0..11 of one wave
-__device__ __forceinline__ void ss_publish(const LaunchArgs &a, int p, int k) {
-    const int lane = threadIdx.x & 63;
-    if (lane < 12) {
-        const double v = k == SS_DONE_K ? 0.0 : S().Ret[k & 1][lane];
-        ss_put(ss_pose_rsrc(a, p), lane * 16, v, ss_tag(a.sstag, k));
-    }
-}
-// main, non-tail waves after barrier 1 of evaluation k: the helper's records of k into idle slots
-__device__ __forceinline__ void ss_fill(const LaunchArgs &a, const PC &q, int mmax, int k, long long &ngath) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nf = nwaves() - TAIL_ROLES;
-    const __amdgpu_buffer_rsrc_t rr = ss_rec_rsrc(a, q.prob);
-    const unsigned long long tag = ss_tag(a.sstag, k);
-    const int *tex = lds_tex(mmax, true);
-    int *tex2 = lds_tex2(mmax, true);
-    const int *slot = lds_slot(mmax, true);
-    double *rec = lds_rec(mmax), *rec2 = lds_rec2(mmax);
-    const int rs = lds_rs(mmax);
-    for (int blk = wave - TAIL_ROLES; blk * 64 < q.M; blk += nf) {
-        // one round trip: the block's count granule (every lane) and entry `lane`'s 8 granules
-        const int base = blk * SS_BLK * 8;
-        const int e = lane < SS_CAP ? lane : 0;
-        const ss_u32x4 cg = ss_get(rr, base);
-        ss_u32x4 g[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = ss_get(rr, base + (1 + e) * SS_ENT * 8 + j * 16);
-        const int cnt = ss_tagof(cg) == tag ? (int)ss_val(cg) : 0;
-        bool ok = lane < cnt;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ok &= ss_tagof(g[j]) == tag;
-        const int i = blk * 64 + (ok ? (int)ss_val(g[0]) : 0);
-        const int tx = ok ? (int)ss_val(g[1]) : -1;
-        ok &= i < q.M;
-        const int ii = ok ? i : 0;
-        const int cur = tex[ii], t2 = tex2[ii], sl = slot[ii];
-        ok &= tx >= 0 && tx != cur && tx != t2;
-        if (ok) {
-            double *dst = (sl ? rec : rec2) + ii;  // the point's idle slot
-#pragma unroll
-            for (int f = 0; f < 6; ++f) dst[(size_t)f * rs] = ss_val(g[2 + f]);
-            tex2[ii] = tx;
-        }
-        const int nok = __popcll(__ballot(ok));
-        ngath += nok;
-        if (q.dbg & 64) ngath += (long long)nok << 32;  // (FMPNP_DBG bit 6: the helper-served ones)
-    }
-}
-// the helper workgroup of problem p (blockIdx after the main and first-evaluation helper grids)
-template <typename T>
-__device__ __forceinline__ void ss_helper_run(const LaunchArgs &a, int mmax) {
-    const int p = (int)blockIdx.x - (a.grid_main + a.n * a.helpers);
-    if (p < 0 || p >= a.n) return;
-    problem_begin(a.probs + p, p, mmax);
-    PC q = load_pc();
-    q.G = 1;
-    q.c0 = q.p0 = 0;
-    q.spec = 1;
-    q.no_memo = 0;
-    q.helpers = q.hfirst = 0;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const double *X = lds_X(mmax);
-    double *rec = lds_rec(mmax);
-    float *qp = lds_qp(mmax, true);
-    const int rs = lds_rs(mmax);
-    const __amdgpu_buffer_rsrc_t pr = ss_pose_rsrc(a, p), rr = ss_rec_rsrc(a, p);
-    const int e6 = 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
-    const bool wlane = (lane & 3) == 0 && e6 < 6;
-    const size_t fo = (size_t)(wlane ? e6 : 0) * rs;
-    for (int k = 0;; ++k) {
-        // evaluation k's pose or a later one (a helper that fell behind skips ahead), or "done";
-        // wave 0 polls (one poller per helper: 128 of them must not load the memory system) and
-        // hands the pose over in LDS; bounded: 0.2 s without a pose ends the helper (results
-        // never depend on it)
-        LMState &st = S();
-        if (wave == 0) {
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            int got = -1;
-            double pv = 0.0;
-            while (true) {
-                const ss_u32x4 g = ss_get(pr, (lane < 12 ? lane : 0) * 16);
-                const unsigned long long tg = ss_tagof(g);
-                const int kk = (tg & ~0xFFFFull) == a.sstag ? (int)(tg & 0xFFFF) - 1 : -1;
-                const int k0 = __builtin_amdgcn_readfirstlane(kk);
-                const bool same = __ballot(lane < 12 && kk != k0) == 0;
-                if (same && k0 == SS_DONE_K) break;
-                if (same && k0 >= k) {
-                    got = k0;
-                    pv = ss_val(g);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(8);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) break;
-            }
-            if (lane < 12) st.Ret[0][lane] = pv;
-            if (lane == 0) st.sc[0].n_evals = got;  // (the helper's own scratch: -1 = stop)
-        }
-        __syncthreads();
-        k = S().sc[0].n_evals;
-        if (k < 0) return;
-        double Re[9], te[3];
-#pragma unroll
-        for (int j = 0; j < 9; ++j) Re[j] = st.Ret[0][j];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) te[j] = st.Ret[0][9 + j];
-        __syncthreads();  // (every wave has its copy before wave 0 writes the next pose)
-        const unsigned long long tag = ss_tag(a.sstag, k);
-        for (int blk = wave; blk * 64 < q.M; blk += nwaves()) {
-            const int i = blk * 64 + lane;
-            const bool valid = i < q.M;
-            int off = -1, pred = -1;
-            float urg = INFINITY;
-            if (valid) {
-                double Pc[3];
-                transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
-                int x, y;
-                double qx, qy;
-                if (project_pc(q, Pc, x, y, qx, qy)) {
-                    const int row = (int)udiv((unsigned)y * (unsigned)q.Hf, q.dh);
-                    const int col = (int)udiv((unsigned)x * (unsigned)q.Wf, q.dw);
-                    off = row * q.Wf + col;
-                    float qpx = qp[i], qpy = qp[mmax + i];
-                    pred = spec_target_u(q, qx, qy, row, col, &qpx, &qpy, urg);
-                    qp[i] = qpx;
-                    qp[mmax + i] = qpy;
-                }
-            }
-            if (!(pred >= 0 && pred != off)) urg = INFINITY;
-            // the block's (at most) ss_cap most urgent predictions (the gathers cost HBM bandwidth
-            // the mains' own misses compete for)
-            unsigned long long m = 0;
-            for (int n = 0; n < a.ss_cap; ++n) {
-                float u = urg;
-                u = fminf(u, __shfl_xor(u, 1));
-                u = fminf(u, __shfl_xor(u, 2));
-                u = fminf(u, __shfl_xor(u, 4));
-                u = fminf(u, __shfl_xor(u, 8));
-                u = fminf(u, __shfl_xor(u, 16));
-                u = fminf(u, __shfl_xor(u, 32));
-                if (!(u < INFINITY)) break;
-                const unsigned long long hit = __ballot(urg == u);
-                const unsigned long long one = hit & (~hit + 1);
-                m |= one;
-                if ((one >> lane) & 1ull) urg = INFINITY;
-            }
-            if (m) {
-                const RecDst rd{rec + fo + blk * 64, rec + fo + blk * 64, 0ull};
-                gather_records<T, true, false>(q, m, pred, 0, blk, rd, wlane);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            }
-            const int base = blk * SS_BLK * 8;
-            if (a.ss != 1) {  // (prefetch-only: the gathers left the texels in this XCD's L2)
-                if (m && lane == 0) rec[(size_t)7 * rs + blk * 64] = 0.0;
-                continue;
-            }
-            if ((m >> lane) & 1ull) {
-                const int e = __popcll(m & ((1ull << lane) - 1));
-                const int eb = base + (1 + e) * SS_ENT * 8;
-                ss_put(rr, eb, (double)lane, tag);
-                ss_put(rr, eb + 16, (double)pred, tag);
-#pragma unroll
-                for (int f = 0; f < 6; ++f) ss_put(rr, eb + 32 + 16 * f, rec[(size_t)f * rs + i], tag);
-            }
-            if (lane == 0) ss_put(rr, base, (double)__popcll(m), tag);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------
 // Specialised per launch (the launcher picks the variant): TEAM = G > 1, RATIO = the ratio
 // test is on, VAR = VAR_GM (Geman-McClure forward, nearest sampling: the common case),
 // VAR_NEAREST (any loss / mode, nearest) or VAR_BILINEAR -- constant-folding the other
 // paths out shortens the per-point code and frees registers.
-// (FMPNP_LAT_WAVES: waves per SIMD the latency build is compiled for -- 2, up to 256 VGPRs; 4 caps it at
-// 128 VGPRs so that two 512-thread workgroups share a CU: the occupancy experiment of DESIGN.md 4.1.4)
-#ifndef FMPNP_LAT_WAVES
-#define FMPNP_LAT_WAVES 2
-#endif
 template <typename T, int WPS, bool TEAM, bool RATIO, int VAR>
 __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
-                             WPS == WPS_WIDE ? 1 : WPS == WPS_LATENCY ? FMPNP_LAT_WAVES : 2) void lm_kernel(LaunchArgs a) {
+                             WPS == WPS_WIDE ? 1 : 2) void lm_kernel(LaunchArgs a) {
     LMState &st = S();
     const int G = a.G;
     // XCD-aware team placement: members of one team share blockIdx % gw (the same XCD
@@ -2760,10 +2504,9 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
     const int b = blockIdx.x, gw = a.gw;
     const int grp = b / (gw * G), rem = b % (gw * G);
     const int s = rem / gw;
-    // first-evaluation helpers (helper_run), then the steady-state gather helpers (ss_helper_run)
-    const bool ss_helper = a.ss != 0 && b >= a.grid_main + a.n * a.helpers;
-    const bool helper = !ss_helper && a.helpers > 0 && b >= a.grid_main;
-    const int team = (helper || ss_helper) ? 0 : grp * gw + rem % gw;
+    // first-evaluation helpers (helper_run) after the main grid
+    const bool helper = a.helpers > 0 && b >= a.grid_main;
+    const int team = helper ? 0 : grp * gw + rem % gw;
     if (team >= a.teams) return;
     const int tid = threadIdx.x;
     const int mmax = a.mmax;
@@ -2809,18 +2552,13 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
         st.stamp_t[tid >> 6] = __builtin_amdgcn_s_memtime();
     }
 #endif
-    constexpr bool kSS = WPS == WPS_LATENCY && !TEAM && (VAR == VAR_GM_SS || VAR == VAR_NEAREST_SS);
     constexpr bool kHelp = WPS == WPS_LATENCY && !TEAM && (VAR == VAR_GM_SPEC_H || VAR == VAR_NEAREST_SPEC_H ||
                                                            VAR == VAR_GM_H || VAR == VAR_NEAREST_H ||
-                                                           VAR == VAR_GM_H_W || VAR == VAR_NEAREST_H_W || kSS);
+                                                           VAR == VAR_GM_H_W || VAR == VAR_NEAREST_H_W);
     // the packed-window check (fmpnp_problem.window on the f, gx, gy planes)
     constexpr bool kWin = VAR == VAR_GM_W || VAR == VAR_NEAREST_W || VAR == VAR_GM_H_W || VAR == VAR_NEAREST_H_W;
     if (helper) {
         if constexpr (kHelp) helper_run<T>(a, mmax);
-        return;
-    }
-    if (ss_helper) {
-        if constexpr (kSS) ss_helper_run<T>(a, mmax);
         return;
     }
     for (int p = team; p < a.n; p += a.teams) {
@@ -2830,13 +2568,12 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
         // the ratio test with a guessed limit (ratio_guess_check): one workgroup per problem, nearest
         constexpr bool kRatio1 = RATIO && !TEAM && VAR != VAR_BILINEAR;
         constexpr bool kSpec = kSpecBuild && WPS == WPS_LATENCY &&
-                               (kSS || VAR == VAR_GM_SPEC || VAR == VAR_NEAREST_SPEC || VAR == VAR_GM_SPEC_H ||
+                               (VAR == VAR_GM_SPEC || VAR == VAR_NEAREST_SPEC || VAR == VAR_GM_SPEC_H ||
                                 VAR == VAR_NEAREST_SPEC_H);
         // the problem's constants in registers (from the LDS Ctx), with this variant's constants
         auto make_q = [&]() {
             PC r = load_pc();
             r.helpers = kHelp ? a.helpers : 0;
-            r.ss_fill = a.ss == 1 ? 1 : 0;
             r.prob = p;
             r.hrec = a.hrec;
             r.hflag = a.hflag;
@@ -2851,11 +2588,10 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
                 r.p0 = 0;
             }
             r.use_ratio = RATIO ? 1 : 0;
-            r.r1 = 1;
             r.spec = kSpec ? 1 : 0;
             if constexpr (kSpec) r.no_memo = 0;
             if constexpr (VAR == VAR_GM || VAR == VAR_F_GM || VAR == VAR_GM_SPEC || VAR == VAR_GM_SPEC_H ||
-                          VAR == VAR_GM_H || VAR == VAR_GM_SS || VAR == VAR_GM_W || VAR == VAR_GM_H_W)
+                          VAR == VAR_GM_H || VAR == VAR_GM_W || VAR == VAR_GM_H_W)
                 r.loss = FMPNP_GEMAN_MCCLURE;
             r.bilinear = (VAR == VAR_BILINEAR || VAR == VAR_BIL_DIRECT) ? 1 : 0;
             return r;
@@ -2874,19 +2610,11 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
                 const int2 dn = *reinterpret_cast<const int2 *>(&st.sc[k & 1].done);
                 if ((dn.x | dn.y) != 0) break;
             }
-            // the steady-state helper's pose of this evaluation (the last wave: off the tail)
-            if constexpr (kSS)
-                if (a.ss && (tid >> 6) == nwaves() - 1) ss_publish(a, p, k);
             if (ev_stamps && tid == 0 && p == team && k < 63) ev_stamps[k] = __builtin_amdgcn_s_memtime();
             q.cur_ev = q.cur_eval = k;
             tl_stamp(q, 0);
             q.hfirst = first_eval && q.helpers > 0 && p == team;  // helpers serve each team's first problem
             first_eval = false;
-            // the ratio test's form for this evaluation: the guessed limit after an evaluation that
-            // gathered at least a.ratio_gthr texels (its pass 1 has the slack to hide the early partials),
-            // else the two passes -- both give the same partials bit for bit (ratio_guess_check)
-            if constexpr (kRatio1 && FMPNP_RATIO_FORMS)
-                q.r1 = (k == 0 || a.ratio_gthr <= 0 || ufirst(st.gcnt[(k + 1) & 1]) >= a.ratio_gthr) ? 1 : 0;
             // project, gather, loss (+ partials)
             // (double-buffered gathers in both builds; speculation in the latency build only)
             // (bilinear: the cell memo; VAR_BIL_DIRECT samples every point at every evaluation)
@@ -2894,25 +2622,21 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
             if constexpr (VAR == VAR_BILINEAR)
                 lmax = eval_pass_bil<T>(q, mmax, ngath);
             else
-                lmax = eval_pass<T, true, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST), kSpec, kHelp, kSS, kRatio1, kWin>(
+                lmax = eval_pass<T, true, (VAR == VAR_F_GM || VAR == VAR_F_NEAREST), kSpec, kHelp, kRatio1, kWin>(
                     q, mmax, ngath, pose);
             // the ratio test: with one workgroup per problem of at most 8 blocks, the guessed limit
             // (ratio_guess_check, after barrier 1); otherwise the two passes (exchange, contrib_pass)
-            const bool r1 = kRatio1 && q.use_ratio && q.M <= 8 * 64 && (!FMPNP_RATIO_FORMS || q.r1);
+            const bool r1 = kRatio1 && q.use_ratio && q.M <= 8 * 64;
             if (q.use_ratio && !r1) {
                 if (!ratio_exchange(lmax)) break;
                 const double limit = ufirst(st.rho_max) * st.c.ratio_thr;
                 contrib_pass(q, mmax, limit);
-                // (the next evaluation's guess, should it take the guessed form)
-                if (FMPNP_RATIO_FORMS && kRatio1 && tid == 0) st.rguess[(k + 1) & 1] = isnan(limit) ? INFINITY : limit;
             }
             const int wave = tid >> 6;
             constexpr bool FLV = VAR == VAR_F_GM || VAR == VAR_F_NEAREST;
             tl_stamp(q, 4);
             if (TEAM) team_arrive();
             else __syncthreads();
-            // (every wave read the previous evaluation's count at this evaluation's start)
-            if (FMPNP_RATIO_FORMS && kRatio1 && tid == 0) st.gcnt[(k + 1) & 1] = 0;
             if (r1) {
                 // (FMPNP_DBG bit 5: every block re-formed -- the two-pass partials, for A/B tests;
                 // bit 6: the re-formed blocks counted in texel_gathers' high word)
@@ -2948,10 +2672,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
             // in the tail, and waves 4-7; waves 1 and 2 after their tail roles when spec_w0 <= 2), and
             // with spec_w0 = 0 wave 3 for wave 0's blocks too.  Their channel sums then leave the next
             // evaluation's point phase, which issue-bounds the SIMDs.
-            if (kSS && a.ss == 1) {
-                // the steady-state helper's records of this evaluation into the idle slots
-                if (wave >= TAIL_ROLES) ss_fill(a, q, mmax, k, ngath);
-            } else if (kSpec && q.spec) {
+            if (kSpec && q.spec) {
                 if (wave >= 1 && wave >= q.spec_w0) {
                     spec_pass<T, WPS == WPS_LATENCY, FLV>(q, mmax, ngath, -1, q.spec_cap);
                     dbg_stamp(q.stamps, 4);  // the speculative gathers
@@ -2966,8 +2687,6 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
             ++k;
         }
         if (ev_stamps && tid == 0 && p == team && k < 64) ev_stamps[k] = __builtin_amdgcn_s_memtime();
-        if constexpr (kSS)
-            if (a.ss && (tid >> 6) == nwaves() - 1) ss_publish(a, p, SS_DONE_K);  // the helper may stop
         // texel gathers of the problem: a team's members add their waves' counts to the zeroed
         // result (G > 1); one workgroup sums its waves' counts in LDS and stores the total with
         // the other result fields (G = 1: the launch needs no memset)

@@ -330,9 +330,7 @@ int fmpnp_last_launch(int *teams, int *wgs_per_problem, int *grid, int *lds_byte
 #define FMPNP_VAR_NEAREST_SPEC_H 9
 #define FMPNP_VAR_GM_H 10
 #define FMPNP_VAR_NEAREST_H 11
-#define FMPNP_VAR_GM_SS 12         /* GM_SPEC with the steady-state gather helpers: one helper workgroup
-                                      per problem gathers the predicted next texels every evaluation */
-#define FMPNP_VAR_NEAREST_SS 13    /* ... and for any loss */
+/* (12 and 13 are retired: the steady-state gather helpers, measured slower and removed) */
 #define FMPNP_VAR_GM_W 14          /* GM / NEAREST / GM_H / NEAREST_H with the packed-window check compiled */
 #define FMPNP_VAR_NEAREST_W 15     /* in (fmpnp_problem.window on the packed f/gx/gy planes: fmpnp_feature_pnp's */
 #define FMPNP_VAR_GM_H_W 16        /* windowed packs); the other packed variants carry no check */

@@ -323,37 +323,6 @@ def test_helpers_that_never_publish_change_nothing(monkeypatch):
     np.testing.assert_array_equal(tb["n_supported"], tr["n_supported"])
 
 
-@pytest.mark.parametrize("B,init,ratio,loss", [(128, "easy", None, "gm"), (128, "hard", None, "gm"),
-                                               (1, "easy", None, "gm"), (128, "easy", 0.8, "gm"),
-                                               (16, "hard", 0.8, "gm"), (128, "easy", None, "cauchy")])
-def test_steady_helpers_change_nothing(B, init, ratio, loss, monkeypatch):
-    """The opt-in steady-state gather helpers (FMPNP_SS=1, VAR_GM_SS: one helper workgroup per
-    query predicts and gathers the next evaluation's texels on an idle CU; =2: they only prefetch)
-    move work, never a result: poses, costs, the schedule and the per-evaluation support are
-    bit-identical to the speculating variant, over repeated launches (the hand-off's tags are
-    launch-unique).  Compiled only into a -DFMPNP_SS=1 build (measured slower)."""
-    if b"steady_helpers=1" not in _lib.load().fmpnp_build_info():
-        pytest.skip("steady-state helpers not compiled in (make EXTRA=-DFMPNP_SS=1)")
-    probs = [packed_problem(synth.problem_inputs(512, 256, 240, 320, seed=q, device=DEV, init=init))
-             for q in range(B)]
-    code, var = (_lib.GEMAN_MCCLURE, "GM") if loss == "gm" else (_lib.CAUCHY, "NEAREST")
-    o = rf.make_options(ITERS, 0.01, code, ratio_threshold=ratio, dtype=_lib.F32)
-    monkeypatch.delenv("FMPNP_SS", raising=False)
-    base, tb = rf.refine(probs, o, trace=True)
-    assert _lib.last_launch()["variant_name"] in (var + "_SPEC", var + "_SPEC_H")
-    for mode in ("1", "2", "1"):
-        monkeypatch.setenv("FMPNP_SS", mode)
-        res, tr = rf.refine(probs, o, trace=True)
-        assert _lib.last_launch()["variant_name"] == var + "_SS"
-        for q in range(B):
-            assert np.array_equal(res[q]["R"], base[q]["R"]) and np.array_equal(res[q]["t"], base[q]["t"]), q
-            assert res[q]["best_cost"] == base[q]["best_cost"] and res[q]["n_evals"] == base[q]["n_evals"], q
-            assert res[q]["status"] & ~_lib.STATUS_HELPER_WAIT == 0
-            np.testing.assert_array_equal(tr[q]["cost"], tb[q]["cost"])
-            np.testing.assert_array_equal(tr[q]["n_supported"], tb[q]["n_supported"])
-            np.testing.assert_array_equal(tr[q]["n_kept"], tb[q]["n_kept"])
-
-
 @pytest.mark.parametrize("B,init,ratio", [(128, "easy", 0.8), (128, "hard", 0.8), (16, "easy", 0.5), (1, "hard", 0.8),
                                           (512, "easy", 0.8)])
 def test_ratio_guess_changes_nothing(B, init, ratio, monkeypatch):
@@ -398,25 +367,3 @@ def test_cfg0_toy_shape_against_oracle(B):
         oracle = list(ex.map(lambda h: oracle_run(h, n_iters=20, loss="squared"), hosts))
     for q in range(B):
         check(res[q], trs[q], *oracle[q], f"toy query {q}")
-
-
-@pytest.mark.parametrize("B,init,ratio", [(128, "easy", 0.8), (128, "hard", 0.8), (16, "easy", 0.5), (1, "hard", 0.8)])
-def test_ratio_form_choice_changes_nothing(B, init, ratio, monkeypatch):
-    """The ratio variants choose per evaluation between the guessed limit and the two passes
-    (FMPNP_RATIO_GTHR: the guess after an evaluation of at least that many texel gathers).  Both
-    forms give the same partials, so any choice gives the same poses, costs, support and kept counts."""
-    if b"ratio_forms=1" not in _lib.load().fmpnp_build_info():
-        pytest.skip("per-evaluation ratio forms are compiled only into a -DFMPNP_RATIO_FORMS=1 build")
-    probs = [packed_problem(synth.problem_inputs(512, 256, 240, 320, seed=40 + q, device=DEV, init=init))
-             for q in range(B)]
-    o = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, ratio_threshold=ratio, dtype=_lib.F32)
-    monkeypatch.setenv("FMPNP_RATIO_GTHR", "0")  # always the guessed limit
-    base, tb = rf.refine(probs, o, trace=True)
-    for thr in ("1000000000", "20", "1"):  # the two passes after evaluation 0; switching; mostly the guess
-        monkeypatch.setenv("FMPNP_RATIO_GTHR", thr)
-        res, tr = rf.refine(probs, o, trace=True)
-        for q in range(B):
-            assert np.array_equal(res[q]["R"], base[q]["R"]) and np.array_equal(res[q]["t"], base[q]["t"]), (thr, q)
-            assert res[q]["best_cost"] == base[q]["best_cost"] and res[q]["n_evals"] == base[q]["n_evals"], (thr, q)
-            np.testing.assert_array_equal(tr[q]["cost"], tb[q]["cost"])
-            np.testing.assert_array_equal(tr[q]["n_kept"], tb[q]["n_kept"])

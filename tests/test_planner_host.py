@@ -57,27 +57,6 @@ def test_headline_plan():
     assert i["lds_bytes"] <= 160 * 1024
 
 
-def test_steady_helpers_opt_in(monkeypatch):
-    """FMPNP_SS=1|2 plans the steady-state gather helpers (one per query on a spare CU); they stay
-    off without a spare CU per problem and with options.helpers < 0 (a shared device).  Only in a
-    -DFMPNP_SS=1 build; the default build never plans them."""
-    monkeypatch.setenv("FMPNP_SS", "1")
-    if b"steady_helpers=1" not in _lib.load().fmpnp_build_info():
-        i = plan(128, rf.make_options(**GM))
-        assert (i["grid"], i["variant_name"]) == (128, "GM_SPEC")
-        return
-    i = plan(128, rf.make_options(**GM))
-    assert (i["grid"], i["variant_name"], i["helpers"]) == (256, "GM_SS", 0)
-    i = plan(128, rf.make_options(**dict(GM, loss=_lib.CAUCHY)))
-    assert i["variant_name"] == "NEAREST_SS"
-    i = plan(1, rf.make_options(**GM))
-    assert i["variant_name"] == "GM_SS" and i["helpers"] >= 2 and i["grid"] == 1 + i["helpers"] + 1
-    i = plan(128, rf.make_options(helpers=-1, **GM))
-    assert (i["grid"], i["variant_name"]) == (128, "GM_SPEC")
-    i = plan(200, rf.make_options(**GM))
-    assert (i["grid"], i["variant_name"]) == (200, "GM_SPEC")
-
-
 def test_single_query_takes_helpers():
     i = plan(1, rf.make_options(**GM))
     assert i["wgs_per_problem"] == 1 and i["helpers"] >= 2 and i["variant_name"] == "GM_SPEC_H"
