@@ -13,7 +13,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <map>
+#include <memory>
 #include <mutex>
+#include <tuple>
 
 #include "fmpnp.h"
 #include "fmpnp_internal.h"
@@ -260,15 +263,50 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     return 0;
 }
 
-struct SyncCache {
-    std::mutex mu;
-    int device = -1;
-    void *buf = nullptr;
-    size_t bytes = 0;
-};
-SyncCache g_cache;
-
 }  // namespace
+
+namespace fmpnp {
+
+StreamScratch *stream_scratch(int pool, hipStream_t s, int *dev_out) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    if (dev_out) *dev_out = dev;
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, uintptr_t>, std::unique_ptr<StreamScratch>> pools;
+    std::lock_guard<std::mutex> lock(mu);  // (the lookup only: each entry has its own mutex)
+    std::unique_ptr<StreamScratch> &e = pools[std::make_tuple(pool, dev, (uintptr_t)s)];
+    if (!e) e.reset(new StreamScratch());
+    return e.get();
+}
+
+int scratch_grow(StreamScratch &c, size_t dbytes, size_t hbytes, size_t dmin, hipStream_t s) {
+    if (c.dev_bytes < dbytes) {
+        // (the entry's earlier calls drained this stream before returning: nothing still reads it)
+        if (c.dev) (void)hipFreeAsync(c.dev, s);
+        c.dev = nullptr;
+        c.dev_bytes = 0;
+        const size_t b = std::max(dbytes, dmin);
+        if (hipMallocAsync((void **)&c.dev, b, s) != hipSuccess) {
+            c.dev = nullptr;
+            return FMPNP_ENOMEM;
+        }
+        c.dev_bytes = b;
+    }
+    if (c.host_bytes < hbytes) {
+        if (c.host) (void)hipHostFree(c.host);
+        c.host = nullptr;
+        c.host_bytes = 0;
+        const size_t b = std::max(hbytes, (size_t)1 << 20);
+        if (hipHostMalloc((void **)&c.host, b, hipHostMallocDefault) != hipSuccess) {
+            c.host = nullptr;
+            return FMPNP_ENOMEM;
+        }
+        c.host_bytes = b;
+    }
+    return 0;
+}
+
+}  // namespace fmpnp
 
 extern "C" {
 
@@ -516,45 +554,35 @@ int fmpnp_refine_batch(const fmpnp_problem *probs_host, int n, const fmpnp_optio
     const size_t b_res = align_up(sizeof(fmpnp_result) * n, 256);
     const size_t b_tr = trace ? align_up(sizeof(fmpnp_trace_entry) * (size_t)n * trace_stride, 256) : 0;
     const size_t need = b_probs + b_res + b_tr + P.ws_total;
-    std::lock_guard<std::mutex> lock(g_cache.mu);
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return (int)e;
-    if (g_cache.buf && (g_cache.bytes < need || g_cache.device != dev)) {
-        int cur = dev;
-        (void)hipSetDevice(g_cache.device);
-        (void)hipDeviceSynchronize();
-        (void)hipFree(g_cache.buf);
-        (void)hipSetDevice(cur);
-        g_cache.buf = nullptr;
-        g_cache.bytes = 0;
-    }
-    if (!g_cache.buf) {
-        size_t bytes = std::max(need, (size_t)1 << 20);
-        e = hipMalloc(&g_cache.buf, bytes);
-        if (e != hipSuccess) return FMPNP_ENOMEM;
-        g_cache.bytes = bytes;
-        g_cache.device = dev;
-    }
-    unsigned char *base = (unsigned char *)g_cache.buf;
+    StreamScratch *sc = stream_scratch(SCRATCH_REFINE, s, nullptr);
+    if (!sc) return FMPNP_ENODEV;
+    std::lock_guard<std::mutex> lock(sc->mu);  // (one call at a time on this stream)
+    if (scratch_grow(*sc, need, 0, (size_t)1 << 20, s)) return FMPNP_ENOMEM;
+    unsigned char *base = sc->dev;
     fmpnp_problem *d_probs = (fmpnp_problem *)base;
     fmpnp_result *d_res = (fmpnp_result *)(base + b_probs);
     fmpnp_trace_entry *d_tr = trace ? (fmpnp_trace_entry *)(base + b_probs + b_res) : nullptr;
     void *d_ws = base + b_probs + b_res + b_tr;
-    e = hipMemcpyAsync(d_probs, probs_host, sizeof(fmpnp_problem) * n, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return (int)e;
+    // an error once work is queued: wait for the stream before returning, so that the scratch is never
+    // reused by the next call on this stream while a copy or launch of this one is still in flight
+    auto drain = [s](int code) {
+        (void)hipStreamSynchronize(s);
+        return code;
+    };
+    hipError_t e = hipMemcpyAsync(d_probs, probs_host, sizeof(fmpnp_problem) * n, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return drain((int)e);
     if (d_tr) {
         e = hipMemsetAsync(d_tr, 0, b_tr, s);
-        if (e != hipSuccess) return (int)e;
+        if (e != hipSuccess) return drain((int)e);
     }
     rc = fmpnp_refine_batch_async(d_probs, probs_host, n, P.max_n, opt, d_res, d_tr, trace_stride, d_ws, P.ws_total,
                                   hip_stream);
-    if (rc) return rc;
+    if (rc) return drain(rc);
     e = hipMemcpyAsync(results, d_res, sizeof(fmpnp_result) * n, hipMemcpyDeviceToHost, s);
-    if (e != hipSuccess) return (int)e;
+    if (e != hipSuccess) return drain((int)e);
     if (trace) {
         e = hipMemcpyAsync(trace, d_tr, sizeof(fmpnp_trace_entry) * (size_t)n * trace_stride, hipMemcpyDeviceToHost, s);
-        if (e != hipSuccess) return (int)e;
+        if (e != hipSuccess) return drain((int)e);
     }
     e = hipStreamSynchronize(s);
     return (int)e;

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+#include <mutex>
+
 #include "fmpnp.h"
 
 // Speculative next-texel gathers (fmpnp_lm_impl.h spec_pass; variants VAR_*_SPEC), on the waves
@@ -121,6 +123,24 @@ inline int win_variant(int var) {
     return var == VAR_GM ? VAR_GM_W : var == VAR_NEAREST ? VAR_NEAREST_W : var == VAR_GM_H ? VAR_GM_H_W
          : var == VAR_NEAREST_H ? VAR_NEAREST_H_W : var;
 }
+// Scratch of the synchronous entry points (fmpnp_refine_batch, fmpnp_feature_pnp), one per (entry
+// point, device, stream): SURVEY.md 8b asks for calls that are thread-safe across distinct streams and
+// devices, so calls on different streams (or devices) use different buffers and run concurrently, and
+// calls on one stream serialise on its mutex (held until the call's stream has drained, so no copy of an
+// earlier call still reads the buffers).  Growing frees only the entry's own buffer, stream-ordered on
+// its own stream (no device-wide synchronisation, never another device's memory).
+struct StreamScratch {
+    std::mutex mu;
+    unsigned char *dev = nullptr;   // device memory of the entry's device
+    size_t dev_bytes = 0;
+    unsigned char *host = nullptr;  // pinned staging (fmpnp_feature_pnp)
+    size_t host_bytes = 0;
+};
+enum { SCRATCH_REFINE = 0, SCRATCH_QUERY = 1 };
+// the entry of (pool, current device, stream); *dev_out: the current device.  nullptr on a HIP error.
+StreamScratch *stream_scratch(int pool, hipStream_t s, int *dev_out);
+// at least dbytes of device memory and hbytes of pinned host memory (call with c.mu held); 0 or FMPNP_ENOMEM
+int scratch_grow(StreamScratch &c, size_t dbytes, size_t hbytes, size_t dmin, hipStream_t s);
 int lm_variant(const fmpnp_options &o);
 const void *lm_kernel_ptr(int dtype, int wps, bool team, bool ratio, int var);
 

@@ -33,52 +33,7 @@ namespace {
 
 inline size_t al(size_t x) { return (x + 255) / 256 * 256; }
 
-// Per-process buffers of the one-query path: device memory on the device of the last call and a
-// pinned host staging buffer, both grown on demand and reused (one call at a time: the mutex is
-// held until the call's stream has drained, so no copy of an earlier call is still in flight).
-struct QueryCache {
-    std::mutex mu;
-    int device = -1;
-    unsigned char *dev = nullptr;
-    size_t dev_bytes = 0;
-    unsigned char *host = nullptr;  // pinned
-    size_t host_bytes = 0;
-};
-QueryCache g_q;
 std::atomic<long long> g_window_reruns{0};  // fmpnp_feature_pnp calls re-run fully packed after a window miss
-
-int grow(QueryCache &c, int device, size_t dbytes, size_t hbytes) {
-    if (c.dev && (c.dev_bytes < dbytes || c.device != device)) {
-        int cur = device;
-        (void)hipSetDevice(c.device);
-        (void)hipDeviceSynchronize();
-        (void)hipFree(c.dev);
-        (void)hipSetDevice(cur);
-        c.dev = nullptr;
-        c.dev_bytes = 0;
-    }
-    if (!c.dev) {
-        const size_t b = std::max(dbytes, (size_t)64 << 20);
-        if (hipMalloc((void **)&c.dev, b) != hipSuccess) {
-            c.dev = nullptr;
-            return FMPNP_ENOMEM;
-        }
-        c.dev_bytes = b;
-        c.device = device;
-    }
-    if (c.host_bytes < hbytes) {
-        if (c.host) (void)hipHostFree(c.host);
-        c.host = nullptr;
-        const size_t b = std::max(hbytes, (size_t)1 << 20);
-        if (hipHostMalloc((void **)&c.host, b, hipHostMallocDefault) != hipSuccess) {
-            c.host = nullptr;
-            c.host_bytes = 0;
-            return FMPNP_ENOMEM;
-        }
-        c.host_bytes = b;
-    }
-    return 0;
-}
 
 }  // namespace
 
@@ -171,13 +126,15 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
     const size_t need = up + down + b_feat + b_fref + al(ws) + b_cost + b_win;
 
     hipStream_t s = (hipStream_t)hip_stream;
-    std::lock_guard<std::mutex> lock(g_q.mu);
-    int device = 0;
-    hipError_t e = hipGetDevice(&device);
-    if (e != hipSuccess) return (int)e;
-    int rc = grow(g_q, device, need, up + down);
+    // this stream's scratch (fmpnp_internal.h StreamScratch): the device carve and a pinned staging
+    // buffer, grown on demand and reused; calls on other streams or devices use their own
+    StreamScratch *sc = stream_scratch(SCRATCH_QUERY, s, nullptr);
+    if (!sc) return FMPNP_ENODEV;
+    std::lock_guard<std::mutex> lock(sc->mu);  // (held until this call's stream has drained)
+    int rc = scratch_grow(*sc, need, up + down, (size_t)64 << 20, s);
     if (rc) return rc;
-    unsigned char *d = g_q.dev, *h = g_q.host;
+    hipError_t e = hipSuccess;
+    unsigned char *d = sc->dev, *h = sc->host;
     double *d_inl = (double *)d, *d_pts = (double *)(d + b_inl);
     fmpnp_problem *d_desc = (fmpnp_problem *)(d + b_inl + b_pts);
     fmpnp_result *d_res = (fmpnp_result *)(d + up);
