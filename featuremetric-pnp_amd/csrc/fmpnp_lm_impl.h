@@ -55,6 +55,12 @@ constexpr bool kSpecBuild = FMPNP_SPEC != 0;
 // its flags and pointers would otherwise hold scalar registers across the evaluation loop.
 // (FMPNP_STAMPS itself is defined in fmpnp_internal.h: it also sizes the LDS head)
 constexpr bool kStamps = FMPNP_STAMPS != 0;
+#ifndef FMPNP_VCONST
+#define FMPNP_VCONST 1
+#endif
+#ifndef FMPNP_LANE_NOW
+#define FMPNP_LANE_NOW 1
+#endif
 // dynamic LDS of the LM kernel (the only kernel in this file that uses LDS)
 extern __shared__ __attribute__((aligned(16))) unsigned char lm_lds[];
 
@@ -120,6 +126,20 @@ struct PC {
     int cur_ev;             // the evaluation being run (its pose is Ret[cur_ev & 1], its state sc[cur_ev & 1])
 };
 
+// The lane index, recomputed where it is used (v_mbcnt inside volatile asm: neither hoisted out of the
+// evaluation loop nor merged with another copy).  Lane masks formed from threadIdx.x (lane < 12, lane < NV,
+// ...) are loop invariants the compiler hoists into SGPR pairs, which the kernel's scalar pressure then
+// spills to VGPR lanes: two v_readlane reloads and a wait state per use on the LM tail, against one
+// v_cmp on a fresh lane index.
+__device__ __forceinline__ int lane_now() {
+#if defined(__HIP_DEVICE_COMPILE__) && FMPNP_LANE_NOW
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+#else
+    return (int)(threadIdx.x & 63);
+#endif
+}
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
 // waves of this workgroup: 8 (NT threads, the latency build) or 4 (the throughput build's
 // 256-thread workgroups, two per CU)
@@ -200,6 +220,12 @@ __device__ __forceinline__ PC load_pc() {
     q.M = ufirst(c.M); q.c0 = ufirst(c.c0); q.LC = ufirst(c.LC); q.G = ufirst(c.G);
     q.dh = UDiv{ufirst(c.div_h.m), ufirst(c.div_h.s1), ufirst(c.div_h.s2)};
     q.dw = UDiv{ufirst(c.div_w.m), ufirst(c.div_w.s1), ufirst(c.div_w.s2)};
+#if FMPNP_VCONST
+    // the projection's constants in VGPRs (wave-uniform values, but the kernel's scalar registers are
+    // spilled to VGPR lanes: each SGPR operand of the projection was a v_readlane reload + s_nop)
+    asm volatile("" : "+v"(q.cx), "+v"(q.cy));
+    asm volatile("" : "+v"(q.dh.m), "+v"(q.dh.s1), "+v"(q.dh.s2), "+v"(q.dw.m), "+v"(q.dw.s1), "+v"(q.dw.s2));
+#endif
     q.loss = ufirst(c.mode == FMPNP_MODE_COMPUTE_COST ? (int)FMPNP_SQUARED : c.loss);
     q.no_memo = ufirst(c.no_memo);
     q.spec = ufirst(c.spec);
@@ -246,7 +272,9 @@ __device__ __forceinline__ void tl_stamp(const PC &q, int k) {
 // equals P2 except in the sign of a zero or for a non-finite coordinate, and each of those makes
 // the quotient non-finite or rounds the pixel to -1 either way -- the point is unsupported in
 // both forms, so the support set and every pixel are the reference's.
-__device__ __forceinline__ bool project_pc(const PC &q, const double P[3], int &x, int &y, double &qx, double &qy) {
+// rz: recip(P[2]) (the Jacobian chain's 1/z, geo_of_iz: formed once per point and evaluation)
+__device__ __forceinline__ bool project_pc(const PC &q, const double P[3], int &x, int &y, double &qx, double &qy,
+                                           double &rz) {
     if (q.kstd) {
 #pragma clang fp contract(off)
         const double u0 = q.fx * P[0] + q.cx * P[2];
@@ -254,6 +282,7 @@ __device__ __forceinline__ bool project_pc(const PC &q, const double P[3], int &
         if (q.bilinear) {  // the taps use the unrounded quotients: the reference's exact division
             qx = u0 / P[2];
             qy = u1 / P[2];
+            rz = recip(P[2]);
         } else {
             // Only the rounded pixel matters here: the quotients by one refined reciprocal (within
             // ~3 ulp of the correctly rounded u / z) round to the same integers as the IEEE
@@ -262,6 +291,7 @@ __device__ __forceinline__ bool project_pc(const PC &q, const double P[3], int &
             // take the exact divisions.  So px, py and the support test are the reference's; qx, qy
             // only feed the speculation's next-texel prediction.
             const double z = P[2], r = recip(z);
+            rz = r;
             double ax = u0 * r, ay = u1 * r;
             const double ex = fabs(fabs(ax - rint(ax)) - 0.5), ey = fabs(fabs(ay - rint(ay)) - 0.5);
             const bool fast = fabs(z) > 0x1p-1000 && fabs(z) < 0x1p+1000 && ex > fabs(ax) * 0x1p-49 &&
@@ -283,6 +313,7 @@ __device__ __forceinline__ bool project_pc(const PC &q, const double P[3], int &
     double K[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) K[k] = Kl[k];
+    rz = recip(P[2]);
     return project_px(K, P, q.im_w, q.im_h, x, y, qx, qy);
 }
 __device__ __forceinline__ unsigned char *dyn() { return lm_lds + lds_fixed_bytes(); }
@@ -761,11 +792,12 @@ __device__ __forceinline__ constexpr int h_col(int k) {
 struct Geo {
     double A0[6], A1[6];
 };
-__device__ __forceinline__ Geo geo_of(const PC &q, bool kept, const double Pc[3]) {
+// izk: recip(Pc[2]) (from project_pc); a point that does not contribute takes z = 1, 1 / z = 1
+__device__ __forceinline__ Geo geo_of_iz(const PC &q, bool kept, const double Pc[3], double izk) {
     const double fx = q.fx, fy = q.fy;
     const double P0 = kept ? Pc[0] : 0.0, P1 = kept ? Pc[1] : 0.0, z = kept ? Pc[2] : 1.0;
     // one reciprocal instead of six divisions (Jacobian entries only: last-bit level)
-    const double iz = recip(z);
+    const double iz = kept ? izk : 1.0;
     const double j00 = fx * iz, j02 = ((-fx) * P0 * iz) * iz;
     const double j11 = fy * iz, j12 = ((-fy) * P1 * iz) * iz;
     return Geo{{j00, 0.0, j02, j02 * P1, j00 * z - j02 * P0, -j00 * P1},
@@ -776,7 +808,13 @@ __device__ __forceinline__ void contrib_geo(const PC &q, int mmax, int blk, bool
 __device__ __forceinline__ void contrib_block(const PC &q, int mmax, int blk, bool sup, bool kept, double rho,
                                               double d1, const double *r, int rs, const double Pc[3],
                                               double *dst_g) {
-    contrib_geo(q, mmax, blk, sup, kept, rho, d1, r, rs, geo_of(q, kept, Pc), dst_g);
+    contrib_geo(q, mmax, blk, sup, kept, rho, d1, r, rs, geo_of_iz(q, kept, Pc, recip(Pc[2])), dst_g);
+}
+// ... with the point's recip(Pc[2]) already formed by project_pc
+__device__ __forceinline__ void contrib_block_iz(const PC &q, int mmax, int blk, bool sup, bool kept, double rho,
+                                                 double d1, const double *r, int rs, const double Pc[3], double izk,
+                                                 double *dst_g) {
+    contrib_geo(q, mmax, blk, sup, kept, rho, d1, r, rs, geo_of_iz(q, kept, Pc, izk), dst_g);
 }
 __device__ __forceinline__ void contrib_geo(const PC &q, int mmax, int blk, bool sup, bool kept, double rho,
                                             double d1, const double *r, int rs, const Geo &G, double *dst_g) {
@@ -1666,11 +1704,12 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
             t2 = -1;
             sl = 0;
         }
+        double rzp = 1.0;  // recip(Pc[2]) of the point (the Jacobian chain's 1 / z)
         if (valid) {
             transform_pt(Re, te, X0, X1, X2, Pc);
             int x, y;
             double qx, qy;
-            if (project_pc(q, Pc, x, y, qx, qy)) {
+            if (project_pc(q, Pc, x, y, qx, qy, rzp)) {
                 const int row = (int)udiv((unsigned)y * (unsigned)q.Hf, q.dh);
                 const int col = (int)udiv((unsigned)x * (unsigned)q.Wf, q.dw);
                 off = row * q.Wf + col;
@@ -1814,14 +1853,14 @@ __device__ __forceinline__ double eval_pass(const PC &q, int mmax, long long &ng
                 // the partials with the guessed limit, and the statistics that tell whether the
                 // true limit keeps the same points (ratio_guess_check)
                 const double a = fabs(rho);
-                contrib_block(q, mmax, blk, sup, sup && a < rguess, rho, d1, r, rs, Pc, dst_g);
+                contrib_block_iz(q, mmax, blk, sup, sup && a < rguess, rho, d1, r, rs, Pc, rzp, dst_g);
                 const double bmax = wave_nanmax(sup ? a : -1.0);
                 if (lane == 0) st.rstat[blk] = bmax;
             } else if (sup) {
                 lmax = nanmax(lmax, fabs(rho));
             }
         } else {
-            contrib_block(q, mmax, blk, sup, sup, rho, d1, r, rs, Pc, dst_g);
+            contrib_block_iz(q, mmax, blk, sup, sup, rho, d1, r, rs, Pc, rzp, dst_g);
         }
         dbg_stamp(q.stamps, 2);
         tl_stamp(q, 3);
@@ -1873,8 +1912,8 @@ __device__ __forceinline__ double eval_pass_bil(const PC &q, int mmax, long long
         if (valid) {
             transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
             int x, y;
-            double qx, qy;
-            if (project_pc(q, Pc, x, y, qx, qy)) {
+            double qx, qy, rz_unused;
+            if (project_pc(q, Pc, x, y, qx, qy, rz_unused)) {
                 Taps tp;
                 bilinear_taps(qx, qy, q.Hf, q.Wf, q.im_w, q.im_h, tp);
                 key = tp.key;
@@ -2015,7 +2054,7 @@ __device__ __forceinline__ double ratio_guess_check(const PC &q, int mmax, doubl
 __device__ __forceinline__ double combine_final_wave(int mmax, bool team, bool spec) {
     LMState &st = S();
     const Ctx &c = st.c;
-    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    const int lane = lane_now(), j = lane & 31, h = lane >> 5;
     const int NC = c.NC;
     double t = 0.0;
     if (!team) {
@@ -2241,7 +2280,7 @@ __device__ __forceinline__ Decision lm_decide(double tot, const LMScal &s, int m
 __device__ __forceinline__ void lm_book(const Decision &d, double tot, double pe, int cur, int mode) {
     LMState &st = S();
     const Ctx &c = st.c;
-    const int lane = threadIdx.x & 63;
+    const int lane = lane_now();
     const LMScal &s = st.sc[cur];
     LMScal &o = st.sc[cur ^ 1];
     if (mode == FMPNP_MODE_COMPUTE_COST) {
@@ -2324,7 +2363,7 @@ __device__ __forceinline__ void lm_book(const Decision &d, double tot, double pe
 __device__ __forceinline__ void lm_step_store(const double *hs, double delta[6], bool solved, double lambda,
                                               double lr, const double *base, int nxt) {
     LMState &st = S();
-    const int lane = threadIdx.x & 63;
+    const int lane = lane_now();
     // (the pivoted-LU fallback indexes H by lane: it reads the LDS copy, not a private array)
     if (!solved) lm_step_rows(hs, hs + 21, lambda, lr, delta);
     bool bad = false;
@@ -2354,7 +2393,7 @@ __device__ __forceinline__ double clip_lr(double l) { return l < 1e-3 ? 1e-3 : (
 __device__ __forceinline__ void lm_tail(int role, double tot, const PC &q, int k) {
     LMState &st = S();
     const Ctx &c = st.c;
-    const int lane = threadIdx.x & 63;
+    const int lane = lane_now();
     const int cur = k & 1, nxt = cur ^ 1;
     const int kk = lane < 12 ? lane : 0;
     const LMScal &s = st.sc[cur];
@@ -2452,8 +2491,8 @@ __device__ __forceinline__ void helper_run(const LaunchArgs &a, int mmax) {
             double Pc[3];
             transform_pt(Re, te, X[i], X[rs + i], X[2 * rs + i], Pc);
             int x, y;
-            double qx, qy;
-            if (project_pc(q, Pc, x, y, qx, qy)) {
+            double qx, qy, rz_unused;
+            if (project_pc(q, Pc, x, y, qx, qy, rz_unused)) {
                 const int row = (int)udiv((unsigned)y * (unsigned)q.Hf, q.dh);
                 const int col = (int)udiv((unsigned)x * (unsigned)q.Wf, q.dw);
                 off = row * q.Wf + col;

@@ -8,7 +8,7 @@ from .matrix_utils import matrix_quaternion  # noqa: F401
 from .model import find_inliers, sparseFeaturePnP  # noqa: F401
 from .optimize_feature_pnp import DirectPoseModel, feature_pnp, feature_pnp_multi, optimize_feature_pnp  # noqa: F401
 from .refine import AsyncBatch, PackedFeatures, Problem, make_options, make_problem, pack_features  # noqa: F401
-from . import pipeline, replay  # noqa: F401,E402
+from . import cpu, pipeline, replay  # noqa: F401,E402
 from .pipeline import RefinePipeline  # noqa: F401,E402
 
 __version__ = "0.1.0"

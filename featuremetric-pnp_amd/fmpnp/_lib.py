@@ -80,7 +80,7 @@ EXPORTS = ["fmpnp_abi_version", "fmpnp_build_info", "fmpnp_device_check", "fmpnp
            "fmpnp_gather_reference_batch", "fmpnp_workspace_size", "fmpnp_refine_batch_async", "fmpnp_refine_batch",
            "fmpnp_last_launch", "fmpnp_debug_stamps", "fmpnp_plan", "fmpnp_last_launch_info",
            "fmpnp_pack_features_f_window_batch", "fmpnp_feature_pnp", "fmpnp_compute_cost_async",
-           "fmpnp_feature_pnp_reruns"]
+           "fmpnp_feature_pnp_reruns", "fmpnp_refine_batch_cpu"]
 
 _LIB = None
 
@@ -127,6 +127,10 @@ def load():
     L.fmpnp_refine_batch.argtypes = [ctypes.POINTER(Problem), i, ctypes.POINTER(Options), ctypes.POINTER(Result),
                                      ctypes.POINTER(TraceEntry), i, vp]
     L.fmpnp_refine_batch.restype = i
+    if hasattr(L, "fmpnp_refine_batch_cpu"):  # (A/B builds of earlier sources lack it)
+        L.fmpnp_refine_batch_cpu.argtypes = [ctypes.POINTER(Problem), i, ctypes.POINTER(Options),
+                                             ctypes.POINTER(Result), ctypes.POINTER(TraceEntry), i, i]
+        L.fmpnp_refine_batch_cpu.restype = i
     L.fmpnp_last_launch.argtypes = [ctypes.POINTER(i)] * 4
     L.fmpnp_last_launch.restype = i
     L.fmpnp_plan.argtypes = [ctypes.POINTER(Problem), i, ctypes.POINTER(Options), ctypes.POINTER(LaunchInfo)]

@@ -29,7 +29,7 @@ def source_digest(root=None, flags=""):
         p = os.path.join(root, rel)
         if os.path.isdir(p):
             files += sorted(os.path.join(rel, f) for f in os.listdir(p)
-                            if f.endswith((".hip", ".h")) and os.path.isfile(os.path.join(p, f)))
+                            if f.endswith((".hip", ".h", ".cpp")) and os.path.isfile(os.path.join(p, f)))
         elif os.path.isfile(p):
             files.append(rel)
     h = hashlib.sha256()

@@ -266,6 +266,17 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
 int fmpnp_refine_batch(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt, fmpnp_result *results,
                        fmpnp_trace_entry *trace, int trace_stride, void *hip_stream);
 
+/* CPU twin of fmpnp_refine_batch: the same descriptors, options, results and trace
+ * with HOST pointers -- feat (the packed [Hf][Wf][3][cstride] of fmpnp_pack_features, or the f-only
+ * [Hf][Wf][cstride] of FMPNP_LAYOUT_F), fref and pts3d in host memory.  The LM loop of
+ * sparseFeaturePnP.forward (featurePnP/model.py:245-494; compute_cost :216-243 with
+ * FMPNP_MODE_COMPUTE_COST) on n_threads host threads (0: every core), one problem per thread at a
+ * time.  Nearest sampling only (FMPNP_BILINEAR: FMPNP_EINVAL); no windows.  An explicit CPU entry
+ * point -- the timed CPU baseline and a parity bridge -- never a fallback of the HIP entry points.
+ * Returns 0 or FMPNP_EINVAL. */
+int fmpnp_refine_batch_cpu(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt, fmpnp_result *results,
+                           fmpnp_trace_entry *trace, int trace_stride, int n_threads);
+
 /* One channel level of multilevel_optimization's pyramid (featurePnP/model.py:193-210): the
  * channel range [c_begin, c_end) of the query map (input_configs/default_robotcar.gin:75). */
 typedef struct {
