@@ -544,7 +544,9 @@ __device__ __forceinline__ void problem_begin(const fmpnp_problem *pb, int p, in
 }
 
 // k: the evaluations completed (the state is sc[k & 1])
-__device__ __forceinline__ void problem_end(bool own_gathers, int k, unsigned long long *tl) {
+// miss_aborts: the f-only layout, where a window miss itself raises abort_flag (one workgroup per
+// problem); elsewhere abort_flag means a timed-out team exchange, whatever else happened
+__device__ __forceinline__ void problem_end(bool own_gathers, int k, unsigned long long *tl, bool miss_aborts) {
     LMState &st = S();
 #if FMPNP_STAMPS
     if (tl && (threadIdx.x & 63) == 0)  // debug timeline: this wave's stamps
@@ -552,9 +554,8 @@ __device__ __forceinline__ void problem_end(bool own_gathers, int k, unsigned lo
 #endif
     if (threadIdx.x == 0) {
         LMScal &sc = st.sc[k & 1];
-        if (st.win_miss) {
-            sc.status |= FMPNP_STATUS_WINDOW;  // (f-only layout: one workgroup per problem, nothing else to stop)
-        } else if (st.abort_flag) {
+        if (st.win_miss) sc.status |= FMPNP_STATUS_WINDOW;
+        if (st.abort_flag && !(st.win_miss && miss_aborts)) {
             st.c.dead = 1;
             sc.status |= FMPNP_STATUS_SYNC_TIMEOUT;
         }
@@ -2548,7 +2549,11 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
     const int team = helper ? 0 : grp * gw + rem % gw;
     if (team >= a.teams) return;
     const int tid = threadIdx.x;
+#ifdef FMPNP_MMAX_FIXED  // (measurement build only: every launch must have this mmax)
+    constexpr int mmax = FMPNP_MMAX_FIXED;
+#else
     const int mmax = a.mmax;
+#endif
     if (tid == 0) {
         Ctx &c = st.c;
         c.results = a.results;
@@ -2737,7 +2742,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
             if ((tid & 63) == 0) st.wg_gath[tid >> 6] = ngath;
             __syncthreads();
         }
-        problem_end(!TEAM, k, q.tl);
+        problem_end(!TEAM, k, q.tl, VAR == VAR_F_GM || VAR == VAR_F_NEAREST);
     }
 #if FMPNP_STAMPS
     if (stamps_on && (tid & 63) == 0)

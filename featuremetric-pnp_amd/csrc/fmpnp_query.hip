@@ -175,8 +175,11 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
         if (e != hipSuccess) return drain((int)e);
     }
     // pack (optimize_feature_pnp.py:57,61): the Sobel pack writes channels < C, so a padded
-    // stride is zeroed first; the f-only copy fills the padding itself
-    if (!lay_f && cs != C) {
+    // stride is zeroed first; the f-only copy fills the padding itself.  Not for a windowed attempt:
+    // its unmarked texels are never trusted anyway (a miss re-runs the call), and no kernel reads a
+    // channel >= C (every level's [c_begin, c_end) lies below C), so zeroing the whole map there would
+    // only add the full-map write the window exists to avoid
+    if (!lay_f && cs != C && !win) {
         e = hipMemsetAsync(d_feat, 0, b_feat, s);
         if (e != hipSuccess) return drain((int)e);
     }

@@ -204,8 +204,10 @@ def _feature_pnp_one_call(model, q, r, prediction, K, image_shape, track, levels
 
 
 def optimize_feature_pnp(query_hypercolumns, net, prediction, K, image_shape=None, track=False, feature_pyramid=None,
-                         features="s2dhm", model=None, verbose=False):
-    """optimize_feature_pnp.py:73-91.  Returns (list t, list quaternion, model)."""
+                         features="s2dhm", model=None, verbose=True):
+    """optimize_feature_pnp.py:73-91.  Returns (list t, list quaternion, model).  Prints the reference's
+    "Initial : ..." / "Final : ..." lines (:76, :90) unless verbose=False (the reference always prints
+    them; a consumer that scrapes stdout sees the same lines)."""
     cfg = config.adapter_kwargs()
     image_shape = image_shape if image_shape is not None else cfg.get("image_shape", (1024, 1024))
     if feature_pyramid is None:

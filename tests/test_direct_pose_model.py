@@ -38,7 +38,7 @@ def test_surface_signatures():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["adapter_square", "adapter_pyramid"])
-def test_direct_pose_model_like_the_predictor(name):
+def test_direct_pose_model_like_the_predictor(name, capsys):
     z, meta, pred = _case(name)
     dev = "cuda:0"
     C, Hq, Wq = z["in_query"].shape
@@ -60,6 +60,10 @@ def test_direct_pose_model_like_the_predictor(name):
                                                     feature_pyramid=pyr)
     np.testing.assert_allclose(np.array(quaternion), z["opt_quat"], atol=1e-9)
     np.testing.assert_allclose(np.array(t), z["opt_t"], atol=1e-9)
+    # the reference adapter's progress lines, printed unconditionally (optimize_feature_pnp.py:76,90)
+    out = capsys.readouterr().out.splitlines()
+    assert out[0] == "Initial : {}".format(list(pred.quaternion) + list(pred.matrix[:3, 3]))
+    assert out[-1] == "Final : {}".format(list(quaternion) + list(t))
     # the predictor's CSV row and export (sparse_to_dense_predictor.py:255-257)
     export = np.zeros(8)
     export[1:5], export[5:] = quaternion, t
