@@ -255,6 +255,9 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     P.ws_total = P.ws_counters + P.ws_partials + P.ws_max + P.ws_hrec + P.ws_hflag;
     P.var = P.spec ? spec_variant(lm_variant(*opt)) : lm_variant(*opt);
     if (P.helpers) P.var = help_variant(P.var);
+    // one 512-point workgroup per problem (N in 449..512, fp32): the compile-time carve (B = 128: 0.3222 ->
+    // 0.3174 ms, single query 0.2513 -> 0.2424 ms, interleaved x3, profiles/r06_ab_m512.txt)
+    if (P.mmax == MMAX_512 && G == 1 && P.wps == WPS_LATENCY && opt->dtype == FMPNP_F32) P.var = m512_variant(P.var);
     // (packed windows: the variant with the window check; the f-only variants always carry theirs)
     if (windows && opt->layout == FMPNP_LAYOUT_FGRAD) P.var = win_variant(P.var);
     P.ratio = opt->use_ratio != 0;

@@ -110,6 +110,13 @@ inline int spec_variant(int var) {
 // LaunchArgs::helpers; the headline-size batches run without it and without its code)
 constexpr int VAR_GM_SPEC_H = FMPNP_VAR_GM_SPEC_H, VAR_NEAREST_SPEC_H = FMPNP_VAR_NEAREST_SPEC_H,
               VAR_GM_H = FMPNP_VAR_GM_H, VAR_NEAREST_H = FMPNP_VAR_NEAREST_H;
+// ... and those two compiled for one 512-point workgroup (mmax = 512 at compile time: the LDS carve's
+// offsets are immediates, ~25 fewer scalar registers spilled; fp32 texels, the latency build)
+constexpr int VAR_GM_SPEC_512 = FMPNP_VAR_GM_SPEC_512, VAR_GM_SPEC_H_512 = FMPNP_VAR_GM_SPEC_H_512;
+constexpr int MMAX_512 = 512;
+inline int m512_variant(int var) {
+    return var == VAR_GM_SPEC ? VAR_GM_SPEC_512 : var == VAR_GM_SPEC_H ? VAR_GM_SPEC_H_512 : var;
+}
 inline int help_variant(int var) {
     return var == VAR_GM_SPEC ? VAR_GM_SPEC_H : var == VAR_NEAREST_SPEC ? VAR_NEAREST_SPEC_H
          : var == VAR_GM ? VAR_GM_H : var == VAR_NEAREST ? VAR_NEAREST_H : var;

@@ -18,6 +18,7 @@ static LmFn pick_var(int var) {
         }
         return nullptr;
     }
+    if (var == VAR_GM_SPEC_512 || var == VAR_GM_SPEC_H_512) return nullptr;  // (fp32 texels only)
     if (var == VAR_GM_H || var == VAR_NEAREST_H) {  // first-evaluation helpers without speculation
         if constexpr (WPS == WPS_LATENCY && !TEAM) {
             if (var == VAR_GM_H) return lm_kernel<double, WPS, TEAM, RATIO, VAR_GM_H>;

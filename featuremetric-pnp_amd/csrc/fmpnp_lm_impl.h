@@ -2549,11 +2549,10 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
     const int team = helper ? 0 : grp * gw + rem % gw;
     if (team >= a.teams) return;
     const int tid = threadIdx.x;
-#ifdef FMPNP_MMAX_FIXED  // (measurement build only: every launch must have this mmax)
-    constexpr int mmax = FMPNP_MMAX_FIXED;
-#else
-    const int mmax = a.mmax;
-#endif
+    // the _512 variants: the planner runs them only with a.mmax == 512, and their LDS carve is a
+    // compile-time constant (immediate ds offsets, fewer scalar registers)
+    constexpr bool kM512 = VAR == VAR_GM_SPEC_512 || VAR == VAR_GM_SPEC_H_512;
+    const int mmax = kM512 ? MMAX_512 : a.mmax;
     if (tid == 0) {
         Ctx &c = st.c;
         c.results = a.results;
@@ -2597,6 +2596,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
     }
 #endif
     constexpr bool kHelp = WPS == WPS_LATENCY && !TEAM && (VAR == VAR_GM_SPEC_H || VAR == VAR_NEAREST_SPEC_H ||
+                                                           VAR == VAR_GM_SPEC_H_512 ||
                                                            VAR == VAR_GM_H || VAR == VAR_NEAREST_H ||
                                                            VAR == VAR_GM_H_W || VAR == VAR_NEAREST_H_W);
     // the packed-window check (fmpnp_problem.window on the f, gx, gy planes)
@@ -2613,6 +2613,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
         constexpr bool kRatio1 = RATIO && !TEAM && VAR != VAR_BILINEAR;
         constexpr bool kSpec = kSpecBuild && WPS == WPS_LATENCY &&
                                (VAR == VAR_GM_SPEC || VAR == VAR_NEAREST_SPEC || VAR == VAR_GM_SPEC_H ||
+                                VAR == VAR_GM_SPEC_512 || VAR == VAR_GM_SPEC_H_512 ||
                                 VAR == VAR_NEAREST_SPEC_H);
         // the problem's constants in registers (from the LDS Ctx), with this variant's constants
         auto make_q = [&]() {
@@ -2635,6 +2636,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
             r.spec = kSpec ? 1 : 0;
             if constexpr (kSpec) r.no_memo = 0;
             if constexpr (VAR == VAR_GM || VAR == VAR_F_GM || VAR == VAR_GM_SPEC || VAR == VAR_GM_SPEC_H ||
+                          VAR == VAR_GM_SPEC_512 || VAR == VAR_GM_SPEC_H_512 ||
                           VAR == VAR_GM_H || VAR == VAR_GM_W || VAR == VAR_GM_H_W)
                 r.loss = FMPNP_GEMAN_MCCLURE;
             r.bilinear = (VAR == VAR_BILINEAR || VAR == VAR_BIL_DIRECT) ? 1 : 0;

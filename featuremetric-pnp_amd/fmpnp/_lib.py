@@ -27,7 +27,7 @@ ABI_VERSION = 4
 BUILD_WIDE, BUILD_LATENCY, BUILD_THROUGHPUT = 1, 2, 4
 BUILD_NAMES = {BUILD_WIDE: "wide", BUILD_LATENCY: "latency", BUILD_THROUGHPUT: "throughput"}
 VARIANT_NAMES = ["NEAREST", "GM", "BILINEAR", "F_NEAREST", "F_GM", "BIL_DIRECT", "GM_SPEC", "NEAREST_SPEC",
-                 "GM_SPEC_H", "NEAREST_SPEC_H", "GM_H", "NEAREST_H", "(retired 12)", "(retired 13)", "GM_W", "NEAREST_W",
+                 "GM_SPEC_H", "NEAREST_SPEC_H", "GM_H", "NEAREST_H", "GM_SPEC_512", "GM_SPEC_H_512", "GM_W", "NEAREST_W",
                  "GM_H_W", "NEAREST_H_W"]
 ERRORS = {-1: "EINVAL", -2: "EALIGN", -3: "ENOMEM", -4: "ETOOBIG", -5: "ENODEV", -6: "ERANGE"}
 ERANGE = -6  # fmpnp_feature_pnp: a reference inlier outside the reference map (IndexError)

@@ -341,7 +341,8 @@ int fmpnp_last_launch(int *teams, int *wgs_per_problem, int *grid, int *lds_byte
 #define FMPNP_VAR_NEAREST_SPEC_H 9
 #define FMPNP_VAR_GM_H 10
 #define FMPNP_VAR_NEAREST_H 11
-/* (12 and 13 are retired: the steady-state gather helpers, measured slower and removed) */
+#define FMPNP_VAR_GM_SPEC_512 12    /* GM_SPEC / GM_SPEC_H compiled for a 512-point workgroup (the LDS carve at */
+#define FMPNP_VAR_GM_SPEC_H_512 13  /* compile-time offsets: configs[1]/[2]'s N = 512, fp32); otherwise as those */
 #define FMPNP_VAR_GM_W 14          /* GM / NEAREST / GM_H / NEAREST_H with the packed-window check compiled */
 #define FMPNP_VAR_NEAREST_W 15     /* in (fmpnp_problem.window on the packed f/gx/gy planes: fmpnp_feature_pnp's */
 #define FMPNP_VAR_GM_H_W 16        /* windowed packs); the other packed variants carry no check */

@@ -67,7 +67,7 @@ def test_bench_variant_meets_fp64_golden_tolerances(name):
     res, trs = rf.refine([prob] * B, opts, trace=True)
     info = _lib.last_launch()
     assert (info["build_name"], info["team"], info["dtype_name"], info["grid"]) == ("latency", 0, "f32", B), info
-    assert info["variant_name"] in ("GM_SPEC", "NEAREST_SPEC"), info
+    assert info["variant_name"] in ("GM_SPEC", "NEAREST_SPEC", "GM_SPEC_512"), info
     for q in (0, B - 1):
         r, tr = res[q], trs[q]
         assert r["n_steps"] == int(gold["rec_n"]), name
@@ -98,7 +98,7 @@ def test_cfg2_bench_variant_vs_oracle_to_fp64_tolerances(init):
                                      inp["R0"], inp["t0"]))
     opts = rf.make_options(50, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32)
     res, trs = rf.refine([probs[q % 4] for q in range(128)], opts, trace=True)
-    assert _lib.last_launch()["variant_name"] == "GM_SPEC"
+    assert _lib.last_launch()["variant_name"] == "GM_SPEC_512"
     worst = (0.0, 0.0, 0.0)
     for q, inp in enumerate(inps):
         fm = inp["fmap"].double().cpu().numpy()

@@ -246,12 +246,12 @@ def _oracle_subset(qs, ratio):
         return list(ex.map(one, qs))
 
 
-@pytest.mark.parametrize("B,ratio,build,variant", [(128, None, "latency", "GM_SPEC"),
-                                                   (128, 0.8, "latency", "GM_SPEC"),
+@pytest.mark.parametrize("B,ratio,build,variant", [(128, None, "latency", "GM_SPEC_512"),
+                                                   (128, 0.8, "latency", "GM_SPEC_512"),
                                                    (512, None, "throughput", "GM"),
                                                    (512, 0.8, "throughput", "GM")])
 def test_bench_launch_against_oracle(B, ratio, build, variant):
-    """The headline launch (B = 128: lm_kernel<float, latency, !team, ratio, VAR_GM_SPEC>, grid 128,
+    """The headline launch (B = 128: lm_kernel<float, latency, !team, ratio, VAR_GM_SPEC_512>, grid 128,
     no first-evaluation helpers), its ratio-test form (input_configs/full_robotcar_08.gin:40), and
     the throughput build of B >= 512 (the fixed_total_1024 leg), each as bench.py launches it
     (AsyncBatch), against the oracle (featurePnP/model.py:300-486, n_iters = 50 of model.gin:5)."""

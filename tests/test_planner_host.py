@@ -15,6 +15,11 @@ EINVAL, ETOOBIG = -1, -4
 
 @pytest.fixture(autouse=True)
 def _cus(monkeypatch):
+    # (the library honours FMPNP_PLAN_CUS only without a device: on a host with one, the plans below --
+    # sized for 256 CUs -- hold only on a 256-CU device)
+    import torch
+    if torch.cuda.is_available() and torch.cuda.get_device_properties(0).multi_processor_count != 256:
+        pytest.skip("the planner plans for the device present, which does not have 256 CUs")
     monkeypatch.setenv("FMPNP_PLAN_CUS", "256")
 
 
@@ -53,13 +58,15 @@ def test_headline_plan():
     gathers, no helpers (no two spare CUs per problem)."""
     i = plan(128, rf.make_options(**GM))
     assert (i["wgs_per_problem"], i["grid"], i["build_name"], i["variant_name"], i["helpers"], i["team"]) == \
-        (1, 128, "latency", "GM_SPEC", 0, 0)
+        (1, 128, "latency", "GM_SPEC_512", 0, 0)
     assert i["lds_bytes"] <= 160 * 1024
 
 
 def test_single_query_takes_helpers():
     i = plan(1, rf.make_options(**GM))
-    assert i["wgs_per_problem"] == 1 and i["helpers"] >= 2 and i["variant_name"] == "GM_SPEC_H"
+    assert i["wgs_per_problem"] == 1 and i["helpers"] >= 2 and i["variant_name"] == "GM_SPEC_H_512"
+    i = plan(1, rf.make_options(**GM), N=448)  # (fewer than 449 points: the runtime carve)
+    assert i["variant_name"] == "GM_SPEC_H"
 
 
 def test_two_per_cu_takes_the_throughput_build():
@@ -70,12 +77,18 @@ def test_two_per_cu_takes_the_throughput_build():
     i = plan(384, rf.make_options(**GM))
     assert (i["build_name"], i["variant_name"]) == ("throughput", "GM")
     i = plan(256, rf.make_options(**GM))
-    assert (i["build_name"], i["variant_name"]) == ("latency", "GM_SPEC")
+    assert (i["build_name"], i["variant_name"]) == ("latency", "GM_SPEC_512")
 
 
 def test_ratio_and_variants():
     i = plan(128, rf.make_options(ratio_threshold=0.8, **GM))
-    assert i["ratio"] == 1 and i["variant_name"] == "GM_SPEC"
+    assert i["ratio"] == 1 and i["variant_name"] == "GM_SPEC_512"
+    i = plan(128, rf.make_options(**dict(GM, dtype=_lib.F64)), C=128)  # (the 512-point carve: fp32 texels only)
+    assert i["variant_name"] == "GM_SPEC"
+    i = plan(128, rf.make_options(**GM), N=449)
+    assert i["variant_name"] == "GM_SPEC_512"
+    i = plan(128, rf.make_options(**GM), N=448)
+    assert i["variant_name"] == "GM_SPEC"
     i = plan(128, rf.make_options(**dict(GM, loss=_lib.CAUCHY)))
     assert i["variant_name"] == "NEAREST_SPEC"
     i = plan(128, rf.make_options(sampling="bilinear", **GM))
@@ -134,7 +147,7 @@ def test_windowed_problems_plan_one_workgroup(monkeypatch):
     i = plan(1, o, window=True)
     assert i["wgs_per_problem"] == 1 and i["team"] == 0
     i = plan(128, rf.make_options(**GM))
-    assert i["speculate"] == 1 and i["variant_name"] == "GM_SPEC"
+    assert i["speculate"] == 1 and i["variant_name"] == "GM_SPEC_512"
     i = plan(128, rf.make_options(**GM), window=True)
     assert i["speculate"] == 0 and i["variant_name"] == "GM_W" and i["build_name"] == "latency"
     i = plan(1, rf.make_options(**GM), window=True)  # (one problem: the first-evaluation helpers too)

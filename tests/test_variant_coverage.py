@@ -42,6 +42,8 @@ from fmpnp import _lib, refine as rf, synth  # noqa: E402  (no skip: a missing H
 DEV = "cuda:0"
 ITERS = 50
 N_PTS, C, HF, WF = 128, 16, 48, 64        # small problems: two 64-point blocks, 4x image
+N_512 = 480                               # the _512 recipes: 449..512 points (eight blocks, the last partial)
+M512 = ("gm_spec_512", "gm_spec_h_512")
 LOSSES = {"gm": (_lib.GEMAN_MCCLURE, "geman_mcclure"), "cauchy": (_lib.CAUCHY, "cauchy")}
 
 # recipe name -> (B, loss, mode, sampling, layout, memo, speculate, wgs_per_problem, variant,
@@ -51,6 +53,9 @@ RECIPES = {
     # latency build, one workgroup per problem
     "gm_spec":          (128, "gm", "fwd", "nearest", "fgrad", True, True, 0, "GM_SPEC", "latency", 0),
     "gm_spec_h":        (1, "gm", "fwd", "nearest", "fgrad", True, True, 0, "GM_SPEC_H", "latency", 0),
+    # ... at 512 points per problem (the compile-time carve, fp32 only; N_512 points)
+    "gm_spec_512":      (128, "gm", "fwd", "nearest", "fgrad", True, True, 0, "GM_SPEC_512", "latency", 0),
+    "gm_spec_h_512":    (1, "gm", "fwd", "nearest", "fgrad", True, True, 0, "GM_SPEC_H_512", "latency", 0),
     "nearest_spec":     (128, "cauchy", "fwd", "nearest", "fgrad", True, True, 0, "NEAREST_SPEC", "latency", 0),
     "nearest_spec_h":   (1, "cauchy", "fwd", "nearest", "fgrad", True, True, 0, "NEAREST_SPEC_H", "latency", 0),
     "gm":               (128, "gm", "fwd", "nearest", "fgrad", True, False, 0, "GM", "latency", 0),
@@ -82,7 +87,7 @@ def _cases():
     out = []
     for name, r in RECIPES.items():
         for dt in ("f32", "f64"):
-            if r[4] == "f" and dt == "f64":
+            if (r[4] == "f" or name in M512) and dt == "f64":
                 continue
             for ratio in (None, 0.8):
                 out.append((name, dt, ratio))
@@ -104,21 +109,21 @@ def info_key(info):
 _INPUTS = {}
 
 
-def _inputs(seed):
+def _inputs(seed, n_pts=N_PTS):
     """Device inputs of synthetic query `seed` (cached: cases share them)."""
-    if seed not in _INPUTS:
+    if (seed, n_pts) not in _INPUTS:
         init = "hard" if seed % 2 else "easy"
-        _INPUTS[seed] = synth.problem_inputs(N_PTS, C, HF, WF, seed=1000 + seed, device=DEV, init=init)
-    return _INPUTS[seed]
+        _INPUTS[(seed, n_pts)] = synth.problem_inputs(n_pts, C, HF, WF, seed=1000 + seed, device=DEV, init=init)
+    return _INPUTS[(seed, n_pts)]
 
 
 _PACKED = {}
 
 
-def _problem(seed, dt, layout):
-    key = (seed, dt, layout)
+def _problem(seed, dt, layout, n_pts=N_PTS):
+    key = (seed, dt, layout, n_pts)
     if key not in _PACKED:
-        inp = _inputs(seed)
+        inp = _inputs(seed, n_pts)
         storage = torch.float64 if dt == "f64" else torch.float32
         fm = inp["fmap"].to(storage)
         feats = rf.pack_features(fm, storage=storage, device=DEV, layout=layout)
@@ -127,8 +132,8 @@ def _problem(seed, dt, layout):
     return _PACKED[key]
 
 
-def _oracle(seed, loss_name, ratio, sampling, mode):
-    inp = _inputs(seed)
+def _oracle(seed, loss_name, ratio, sampling, mode, n_pts=N_PTS):
+    inp = _inputs(seed, n_pts)
     fm = inp["fmap"].double().cpu().numpy()
     gx, gy = orc.sobel(fm)
     fref = inp["fref"].double().cpu().numpy()
@@ -149,7 +154,8 @@ def rot_angle(Ra, Rb):
 def test_specialisation_against_oracle(name, dt, ratio):
     B, loss, mode, sampling, layout, memo, spec, wgs, *_ = RECIPES[name]
     code, loss_name = LOSSES[loss]
-    probs = [_problem(q, dt, layout) for q in range(B)]
+    n_pts = N_512 if name in M512 else N_PTS
+    probs = [_problem(q, dt, layout, n_pts) for q in range(B)]
     opts = rf.make_options(ITERS, 0.01, code, ratio_threshold=ratio, dtype=_lib.F64 if dt == "f64" else _lib.F32,
                            mode=_lib.MODE_COMPUTE_COST if mode == "cost" else _lib.MODE_FORWARD,
                            wgs_per_problem=wgs, memoize=memo, sampling=sampling, speculate=spec)
@@ -158,7 +164,7 @@ def test_specialisation_against_oracle(name, dt, ratio):
     assert info_key(info) == case_key(name, dt, ratio), info
     subset = sorted({0, B // 2, B - 1})
     for q in subset:
-        ores, otr = _oracle(q, loss_name, ratio, sampling, mode)
+        ores, otr = _oracle(q, loss_name, ratio, sampling, mode, n_pts)
         r = res[q]
         what = f"{name} {dt} ratio={ratio} query {q}"
         if mode == "cost":
@@ -184,7 +190,7 @@ def _sweep():
     seen = {}
     grid = itertools.product(("f32", "f64"), ("fgrad", "f"), ("nearest", "bilinear"), ("gm", "cauchy"),
                              ("fwd", "cost"), (0, 1, 2), (None, 0.8), (1, 8, 128, 256, 512),
-                             (64, 128, 2048), (16, 512), (0, 2), (0, -1))
+                             (64, 128, 480, 2048), (16, 512), (0, 2), (0, -1))
     for dt, layout, sampling, loss, mode, no_memo, ratio, B, N, Cc, wgs, helpers in grid:
         if layout == "f" and (dt == "f64" or sampling != "nearest"):
             continue

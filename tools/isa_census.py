@@ -2,12 +2,12 @@
 """ISA census of one LM kernel variant by phase (verdict r05 item 1).
 
 Compiles ONE instantiation of lm_kernel (default: the headline, float / latency build / no team /
-no ratio / VAR_GM_SPEC) to gfx950 assembly with -DFMPNP_ISA_MARKS=1, which turns every tl_stamp site of
+no ratio / VAR_GM_SPEC_512) to gfx950 assembly with -DFMPNP_ISA_MARKS=1, which turns every tl_stamp site of
 fmpnp_lm_impl.h into an assembly comment ';@@TL k', then counts the instructions between consecutive
 markers (in layout order) by class.  Straight-line phases (projection, loss, partials, combine,
 solve) are counted exactly; loops (the gathers) are counted once per static copy.
 
-usage: tools/isa_census.py [--var VAR_GM_SPEC] [--ratio 0|1] [--extra '-DFOO=1'] [--out FILE] [--asm FILE]
+usage: tools/isa_census.py [--var VAR_GM_SPEC_512] [--ratio 0|1] [--extra '-DFOO=1'] [--out FILE] [--asm FILE]
 """
 import argparse
 import collections
@@ -104,7 +104,7 @@ def census(asm_path):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--var", default="VAR_GM_SPEC")
+    ap.add_argument("--var", default="VAR_GM_SPEC_512")
     ap.add_argument("--ratio", type=int, default=0)
     ap.add_argument("--extra", default="")
     ap.add_argument("--asm", default=None, help="census an existing .s instead of compiling")
