@@ -60,37 +60,54 @@ def _in_threads(fns):
     return out, wall
 
 
+def _abi_call(probs, opts, stream):
+    """One thread's calls of fmpnp_refine_batch through the C ABI (ctypes releases the GIL for the call):
+    descriptors and result buffers built once, so the loop is the library's own work, not Python's."""
+    import ctypes
+    n = len(probs)
+    descs = (_lib.Problem * n)(*[p.descriptor() for p in probs])
+    o = rf.bind_layout(probs, opts)
+    res = (_lib.Result * n)()
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    L = _lib.load()
+
+    def call(read=True):
+        _lib.check(L.fmpnp_refine_batch(descs, n, ctypes.byref(o), res, None, 0, sp), "fmpnp_refine_batch")
+        return [rf._result_dict(r) for r in res] if read else None
+    return call
+
+
 def test_refine_batch_two_streams_concurrent():
     """Two threads, one stream each, 12 calls of fmpnp_refine_batch each (96 queries per call: two
-    calls fill 192 of the 256 CUs): bit-identical to the serial calls, and faster than them."""
+    calls fill 192 of the 256 CUs): bit-identical to the serial calls, and faster than them (the two
+    streams' launches overlap on the device)."""
     B, reps = 96, 12
     pa, pb = _problems(B, 0), _problems(B, 1000)
     opts = rf.make_options(50, 0.01, _lib.GEMAN_MCCLURE, dtype=_lib.F32)
     sa, sb = torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)
+    ca_, cb_ = _abi_call(pa, opts, sa), _abi_call(pb, opts, sb)
 
-    def calls(probs, stream):
+    def loop(call):
         def f():
-            with torch.cuda.stream(stream):
-                res = None
-                for _ in range(reps):
-                    res, _tr = rf.refine(probs, opts)
-                return res
+            for _ in range(reps - 1):
+                call(read=False)
+            return call()
         return f
-    # warm both streams' scratch, then the serial reference and its time
-    base, _ = _in_threads([calls(pa, sa)])
-    base_b, _ = _in_threads([calls(pb, sb)])
+    # the reference results (and both streams' scratch warmed), then the serial time
+    ra, rb = ca_(), cb_()
+    with torch.cuda.stream(sa):
+        base_a, _ = rf.refine(pa, opts)
+    _same(ra, base_a)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ra = calls(pa, sa)()
-    rb = calls(pb, sb)()
+    loop(ca_)()
+    loop(cb_)()
     serial = time.perf_counter() - t0
-    _same(ra, base[0])
-    _same(rb, base_b[0])
-    (ca, cb), wall = _in_threads([calls(pa, sa), calls(pb, sb)])
-    _same(ca, ra)
-    _same(cb, rb)
+    (la, lb), wall = _in_threads([loop(ca_), loop(cb_)])
+    _same(la, ra)
+    _same(lb, rb)
     print(f"fmpnp_refine_batch, 2 x {reps} calls of B={B}: serial {serial * 1e3:.1f} ms, two threads {wall * 1e3:.1f} ms")
-    assert wall < 0.9 * serial, (wall, serial)
+    assert wall < 0.8 * serial, (wall, serial)
 
 
 def test_refine_batch_one_stream_two_threads_serialise():
