@@ -158,6 +158,10 @@ def compact_line(out, detail_ref):
         pv = cb.get("poses_vs_gpu") or {}
         c["poses_vs_gpu"] = {k: pv[k] for k in ("max_rot_diff_rad", "max_t_diff_m", "within_1e-4") if k in pv}
         c["pytorch_cpu_fp64"] = {k: v.get("value") for k, v in (cb.get("pytorch_cpu_fp64") or {}).items()}
+        if isinstance(cb.get("cpu_twin"), dict):
+            tw = cb["cpu_twin"]
+            c["cpu_twin"] = {"value": tw.get("value"), "cores": tw.get("cores"),
+                             "within_1e-4": (tw.get("poses_vs_gpu") or {}).get("within_1e-4")}
         line["cpu_baseline"] = c
     legs = {}
     for k, v in out.items():
@@ -1020,6 +1024,26 @@ def cpu_baseline(args, res_gpu, synth, dev):
                                 "poses_vs_gpu": cmp(poses)}
     torch.set_num_threads(prev_threads)
     out["pytorch_cpu_fp64"] = tt
+    # (3) the library's CPU twin (fmpnp_refine_batch_cpu, include/fmpnp.h): the GPU's own packed fp32 maps
+    # (the fp64 Sobel of the fp32 map rounded to fp32, as the pack kernel writes them), the LM kernel's
+    # form of the loop on the same host threads -- a strong CPU baseline beside the reference-form port
+    from fmpnp import _lib, cpu as fcpu, refine as rf
+    St = min(S, max(threads, 4))
+    hp = []
+    for inp, fm, gx, gy in maps[:St]:
+        feats = fcpu.pack_host(fm.astype(np.float32), gx.astype(np.float32), gy.astype(np.float32), np.float32)
+        hp.append(fcpu.problem_host(feats, inp["fref"].astype(np.float32), inp["pts3d"], inp["K"], inp["im_width"],
+                                    inp["im_height"], inp["R0"], inp["t0"]))
+    topts = rf.make_options(ITERS, 0.01, _lib.GEMAN_MCCLURE, ratio_threshold=args.ratio, dtype=_lib.F32)
+    n_twin = max(St, 16 * args.cpu_sample)
+    t = time.perf_counter()
+    tres, _ = fcpu.refine_cpu([hp[i % St] for i in range(n_twin)], topts, n_threads=threads)
+    dt = time.perf_counter() - t
+    out["cpu_twin"] = {"value": round(n_twin / dt, 2), "unit": "pose-refinements/s", "cores": threads,
+                       "sample": f"{n_twin} cfg2 problems = {St} distinct queries repeated, 50 iters, GM, the packed "
+                                 f"fp32 maps, fmpnp_refine_batch_cpu on {threads} threads, {dt:.1f}s",
+                       "poses_vs_gpu": cmp([(r["R"], r["t"]) for r in tres[:St]])}
+    del hp
     return out
 
 
