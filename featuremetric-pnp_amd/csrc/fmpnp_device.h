@@ -143,9 +143,14 @@ __device__ __forceinline__ void loss_eval(int loss, double alpha, double x, doub
         // b = x/4 + 1.  b^-1 by a Newton-refined reciprocal (within an ulp of pow's correctly
         // rounded value; rho only enters the mean cost), b^-2 as (1/b)^2.
         const double b = x / 4.0 + 1.0;
+#if FMPNP_GM_POW  // the reference's pow form (A/B only: profiles/r06_gm_pow_ab.txt)
+        rho = -4.0 * (pow(b, -1.0) - 1.0);
+        d1 = pow(b, -2.0);
+#else
         const double r = recip(b);
         rho = -4.0 * (r - 1.0);
         d1 = r * r;
+#endif
     } else {                                                            // :58-68
         double beta_safe = fabs(alpha - 2.0);
         beta_safe = beta_safe < kEpsF32 ? kEpsF32 : beta_safe;

@@ -2052,13 +2052,11 @@ __device__ __forceinline__ double ratio_guess_check(const PC &q, int mmax, doubl
 // h, h+2, h+4, ... in order; the halves are then added.  Depends only on the chunk
 // partials and NC -- not on G, placement or timing.
 // ---------------------------------------------------------------------------
-// NC8: the _512 variants -- eight blocks, a compile-time count (the same loads and adds, no conditions)
-template <bool NC8 = false>
 __device__ __forceinline__ double combine_final_wave(int mmax, bool team, bool spec) {
     LMState &st = S();
     const Ctx &c = st.c;
-    const int lane = lane_now(), j = lane & 31, h = (lane >> 5) & 1;  // (& 1: lane_now() is opaque)
-    const int NC = NC8 ? MMAX_512 / CH : c.NC;
+    const int lane = lane_now(), j = lane & 31, h = lane >> 5;
+    const int NC = c.NC;
     double t = 0.0;
     if (!team) {
         const double *src = lds_part(mmax, spec);
@@ -2709,7 +2707,7 @@ __global__ __launch_bounds__(WPS == WPS_LATENCY ? NT : NT_THROUGHPUT,
                 }
             } else if (wave < TAIL_ROLES) {
                 dbg_stamp(q.stamps, 3);
-                const double tot = combine_final_wave<kM512>(mmax, false, kSpec);
+                const double tot = combine_final_wave(mmax, false, kSpec);
                 dbg_stamp(q.stamps, 4);
                 tl_stamp(q, 6);
                 lm_tail(wave == 0 ? ROLE_ACC : wave == 1 ? ROLE_REJ : ROLE_BOOK, tot, q, k);
