@@ -309,6 +309,14 @@ int scratch_grow(StreamScratch &c, size_t dbytes, size_t hbytes, size_t dmin, hi
     return 0;
 }
 
+int scratch_side(StreamScratch &c) {
+    hipError_t e = hipSuccess;
+    if (!c.side) e = hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i)
+        if (!c.ev[i]) e = hipEventCreateWithFlags(&c.ev[i], hipEventDisableTiming);
+    return (int)e;
+}
+
 }  // namespace fmpnp
 
 extern "C" {

@@ -142,12 +142,18 @@ struct StreamScratch {
     size_t dev_bytes = 0;
     unsigned char *host = nullptr;  // pinned staging (fmpnp_feature_pnp)
     size_t host_bytes = 0;
+    // fmpnp_feature_pnp's second stream on the entry's device (the channels the first level does not read
+    // are packed there, under the first level's LM launch) and its two fences; created on first use
+    hipStream_t side = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
 };
 enum { SCRATCH_REFINE = 0, SCRATCH_QUERY = 1 };
 // the entry of (pool, current device, stream); *dev_out: the current device.  nullptr on a HIP error.
 StreamScratch *stream_scratch(int pool, hipStream_t s, int *dev_out);
 // at least dbytes of device memory and hbytes of pinned host memory (call with c.mu held); 0 or FMPNP_ENOMEM
 int scratch_grow(StreamScratch &c, size_t dbytes, size_t hbytes, size_t dmin, hipStream_t s);
+// the entry's side stream and events (call with c.mu held, on the entry's device); 0 or a hipError_t
+int scratch_side(StreamScratch &c);
 int lm_variant(const fmpnp_options &o);
 const void *lm_kernel_ptr(int dtype, int wps, bool team, bool ratio, int var);
 

@@ -151,13 +151,38 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
     }
     // an error once work is queued: wait for the stream before returning, so the pinned staging buffer
     // and the device carve are never reused (by the next call) while an earlier copy still reads them
-    auto drain = [s](int code) {
+    auto drain = [s, sc](int code) {
         (void)hipStreamSynchronize(s);
+        if (sc->side) (void)hipStreamSynchronize(sc->side);
         return code;
+    };
+    // the first level's channels [sb, se) packed on the main stream and the other channels on the side
+    // stream, under the first level's LM launch (one workgroup and its helpers: the rest of the device is
+    // idle).  Only with channel boundaries on 128-byte lines (sb, se multiples of 32), so no cache line
+    // holds channels of both streams' packs; FMPNP_QUERY_SPLIT=0 switches it off (A/B knob)
+    static const bool split_on = [] { const char *v = getenv("FMPNP_QUERY_SPLIT"); return !(v && *v == '0'); }();
+    const int sb = n_levels >= 2 ? levels[0].c_begin : 0, se = n_levels >= 2 ? levels[0].c_end : C;
+    const bool split = split_on && n_levels >= 2 && !lay_f && (sb > 0 || se < C) && sb % 32 == 0 &&
+                       (se % 32 == 0 || se == C);
+    if (split) {
+        const int rc2 = scratch_side(*sc);
+        if (rc2) return rc2;
+    }
+    // Sobel pack of channels [c0, c1) (fmpnp_pack.hip: a channel's gradients read only its own plane, so a
+    // channel range is the whole-map pack's bytes for those channels) on stream st
+    bool win = false;
+    auto pack_range = [&](int c0, int c1, hipStream_t st) -> hipError_t {
+        const void *src = (const unsigned char *)query_chw + (size_t)c0 * H * W * (dtype_query == FMPNP_F64 ? 8 : 4);
+        void *dst = d_feat + (size_t)c0 * es;
+        if (win)
+            return launch_pack_win(src, dtype_query, c1 - c0, H, W, dst, opt->dtype, cs, opt->sobel_flags & 1,
+                                   (opt->sobel_flags >> 1) & 1, d_win, st);
+        return launch_pack(src, nullptr, nullptr, dtype_query, c1 - c0, H, W, dst, opt->dtype, cs,
+                           opt->sobel_flags & 1, (opt->sobel_flags >> 1) & 1, st, planes);
     };
   for (int attempt = 0; attempt < 2; ++attempt) {
     // attempt 0: windowed when asked; attempt 1 (only after a window miss): the full pack
-    const bool win = attempt == 0 && window_radius > 0;
+    win = attempt == 0 && window_radius > 0;
     if (attempt == 1 && window_radius == 0) break;
     for (int r = 0; r < n_res; ++r) hd[r].window = win ? d_win : nullptr;
     // the one upload
@@ -189,12 +214,9 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
         // start; the LM flags a gather outside the window (FMPNP_STATUS_WINDOW) and the call re-runs
         e = launch_win_mark(d_desc, 1, window_radius, N, (long)H * W, s);
         if (e != hipSuccess) return drain((int)e);
-        e = launch_pack_win(query_chw, dtype_query, C, H, W, d_feat, opt->dtype, cs, opt->sobel_flags & 1,
-                            (opt->sobel_flags >> 1) & 1, d_win, s);
-    } else {
-        e = launch_pack(query_chw, nullptr, nullptr, dtype_query, C, H, W, d_feat, opt->dtype, cs,
-                        opt->sobel_flags & 1, (opt->sobel_flags >> 1) & 1, s, planes);
     }
+    // with a split, only the first level's channels here; the rest on the side stream below
+    e = split ? pack_range(sb, se, s) : pack_range(0, C, s);
     if (e != hipSuccess) return drain((int)e);
     // fref (optimize_feature_pnp.py:51-56): the reference map's first C channels
     if (N > 0) {
@@ -206,16 +228,35 @@ extern "C" int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, 
                               d_err, s);
         if (e != hipSuccess) return drain((int)e);
     }
+    if (split) {
+        // the side stream: after the first level's pack and the fref gather, the other channels' pack and
+        // compute_cost (which reads every channel); the main stream meets it before the second level
+        e = hipEventRecord(sc->ev[0], s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(sc->side, sc->ev[0], 0);
+        if (e == hipSuccess && sb > 0) e = pack_range(0, sb, sc->side);
+        if (e == hipSuccess && se < C) e = pack_range(se, C, sc->side);
+        if (e != hipSuccess) return drain((int)e);
+        e = launch_compute_cost(hd[0], opt->layout, opt->dtype, opt->use_ratio, opt->ratio_threshold, d_cost, d_sup,
+                                d_res, sc->side);
+        if (e == hipSuccess) e = hipEventRecord(sc->ev[1], sc->side);
+        if (e != hipSuccess) return drain((int)e);
+    }
     // the LM launches
     for (int r = 0; r < n_res; ++r) {
         const bool cost = n_levels > 0 && r == 0;
         if (cost) {
             // compute_cost (model.py:216-243): every point's cost at once (one wave each), one
             // fixed-order reduction -- one evaluation, so not an LM launch (a latency chain there)
-            e = launch_compute_cost(hd[0], opt->layout, opt->dtype, opt->use_ratio, opt->ratio_threshold, d_cost, d_sup,
-                                    d_res, s);
+            // (with a split it runs on the side stream, above)
+            if (!split)
+                e = launch_compute_cost(hd[0], opt->layout, opt->dtype, opt->use_ratio, opt->ratio_threshold, d_cost,
+                                        d_sup, d_res, s);
             if (e != hipSuccess) return drain((int)e);
             continue;
+        }
+        if (split && r == 2) {
+            e = hipStreamWaitEvent(s, sc->ev[1], 0);
+            if (e != hipSuccess) return drain((int)e);
         }
         if (n_levels > 0 && r >= 2) {
             // level r - 1 starts from level r - 2's result: R[9], t[3] -> R0[9], t0[3] (contiguous)
