@@ -124,7 +124,8 @@ int make_plan(const fmpnp_problem *probs, int n, const fmpnp_options *opt, Plan 
     static const int spec_maxc = [] { const char *e = getenv("FMPNP_SPEC_MAXC"); return e ? atoi(e) : 0; }();
     const int maxc = spec_maxc > 0 ? spec_maxc : 64 * (16 / elem_size(opt->dtype));  // (measurement knob)
     // packed windows (fmpnp_feature_pnp, the windowed f-only packs): the speculative gathers would read
-    // predicted texels outside the window, so they are off
+    // predicted texels outside the window, so they are off (variants that withdraw such predictions were
+    // measured slower on the RobotCar call, 1.290 -> 1.311 ms: profiles/r06_spec_window_ab.txt)
     bool windows = false;
     for (int i = 0; i < n; ++i) windows = windows || probs[i].window != nullptr;
     P.spec = (FMPNP_SPEC && !windows && opt->no_memo == 0 && opt->sampling == FMPNP_NEAREST &&

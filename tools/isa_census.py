@@ -8,6 +8,7 @@ markers (in layout order) by class.  Straight-line phases (projection, loss, par
 solve) are counted exactly; loops (the gathers) are counted once per static copy.
 
 usage: tools/isa_census.py [--var VAR_GM_SPEC_512] [--ratio 0|1] [--extra '-DFOO=1'] [--out FILE] [--asm FILE]
+                           [--rev GIT_REV]   (--rev: the sources of that revision, e.g. round 5's final)
 """
 import argparse
 import collections
@@ -66,7 +67,7 @@ def classify(op, args):
     return "other"
 
 
-def compile_asm(var, ratio, extra, out_s):
+def compile_asm(var, ratio, extra, out_s, pkg=PKG):
     src = tempfile.NamedTemporaryFile("w", suffix=".hip", delete=False)
     src.write('#include "fmpnp_lm_impl.h"\nnamespace fmpnp {\n'
               f"template __global__ void lm_kernel<float, WPS_LATENCY, false, {'true' if ratio else 'false'}, "
@@ -74,7 +75,7 @@ def compile_asm(var, ratio, extra, out_s):
     src.close()
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", "-I../include", "-Icsrc",
            "-DFMPNP_ISA_MARKS=1", "--cuda-device-only", "-S", src.name, "-o", out_s] + extra.split()
-    subprocess.run(cmd, cwd=PKG, check=True, stderr=subprocess.DEVNULL)
+    subprocess.run(cmd, cwd=pkg, check=True, stderr=subprocess.DEVNULL)
     os.unlink(src.name)
 
 
@@ -109,13 +110,22 @@ def main():
     ap.add_argument("--extra", default="")
     ap.add_argument("--asm", default=None, help="census an existing .s instead of compiling")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--rev", default=None, help="census the sources of this git revision")
     a = ap.parse_args()
     s_path = a.asm or os.path.join(tempfile.gettempdir(), "fmpnp_isa_census.s")
     if not a.asm:
-        compile_asm(a.var, a.ratio, a.extra, s_path)
+        pkg = PKG
+        if a.rev:  # that revision's csrc/ and include/ in a scratch tree
+            tmp = tempfile.mkdtemp()
+            arch = subprocess.run(["git", "-C", ROOT, "archive", a.rev, "featuremetric-pnp_amd/csrc", "include"],
+                                  check=True, capture_output=True).stdout
+            subprocess.run(["tar", "-x", "-C", tmp], input=arch, check=True)
+            pkg = os.path.join(tmp, "featuremetric-pnp_amd")
+        compile_asm(a.var, a.ratio, a.extra, s_path, pkg)
     meta, segs = census(s_path)
     classes = sorted({c for _, cnt in segs for c in cnt})
-    out = [f"# ISA census: lm_kernel<float, WPS_LATENCY, false, {bool(a.ratio)}, {a.var}> {a.extra}".rstrip(),
+    out = [f"# ISA census: lm_kernel<float, WPS_LATENCY, false, {bool(a.ratio)}, {a.var}> {a.extra}".rstrip()
+           + (f" (sources of {a.rev})" if a.rev else ""),
            f"# resources: {meta}",
            "# segments in layout order, each named by the marker that opens it (the code after that tl_stamp "
            "site up to the next marker)"]
