@@ -219,7 +219,7 @@ def workload_tag(B, init, ratio, memo, sampling, layout, spec=True):
     return t
 
 
-PROFILE_ROUNDS = ("r05", "r04", "r03", "r02")  # newest first
+PROFILE_ROUNDS = ("r06", "r05", "r04", "r03", "r02")  # newest first
 
 
 def load_traffic(tag, kernel, digest, root=ROOT):
