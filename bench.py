@@ -37,6 +37,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
        rank 0 prints the line.  Under a launcher (WORLD_SIZE set) --gpus must equal WORLD_SIZE.
 """
 import argparse
+import contextlib
 import gc
 import json
 import math
@@ -771,8 +772,11 @@ def facade_calls(dev, synth, name, calls=24, warmup=2, via="feature_pnp", querie
             return model
         pr = pred_t(p.points_3d, p.reference_inliers, p.matrix, matrix_utils.matrix_quaternion(p.matrix),
                     "reference.png", None)
-        t, quat, model = fmpnp.optimize_feature_pnp(q[None], _StubNet(r), pr, K, image_shape=img, feature_pyramid=pyr,
-                                                    model=model)
+        # (the reference's "Initial : ..." / "Final : ..." prints stay in the timed call, on stderr: stdout
+        # carries only the bench's one JSON line)
+        with contextlib.redirect_stdout(sys.stderr):
+            t, quat, model = fmpnp.optimize_feature_pnp(q[None], _StubNet(r), pr, K, image_shape=img,
+                                                        feature_pyramid=pyr, model=model)
         return model
     from fmpnp import _lib
     for i in range(warmup):
