@@ -28,8 +28,13 @@
  * buffers are caller-owned DEVICE memory; results and traces of the
  * synchronous entry points are host memory.  Every entry point returns 0 on
  * success, a negative FMPNP_E* code for invalid arguments, or a positive
- * hipError_t; nothing throws.  One call per stream at a time; calls on
- * distinct streams / devices are independent.  Multi-GPU = one call per device.
+ * hipError_t; nothing throws.
+ *
+ * Threads: the asynchronous entry points touch only caller-owned memory.  The synchronous ones
+ * (fmpnp_refine_batch, fmpnp_feature_pnp) keep their scratch per (entry point, device, stream), each
+ * behind its own mutex, and drain their stream before returning an error once work is queued: calls
+ * on distinct streams or devices run concurrently, calls on one stream from several threads
+ * serialise.  Multi-GPU = one host thread (or process) per device.
  */
 #ifndef FMPNP_H
 #define FMPNP_H
@@ -262,7 +267,8 @@ int fmpnp_refine_batch_async(const fmpnp_problem *probs_dev, const fmpnp_problem
 
 /* Synchronous convenience: host descriptors in, host results (and optional
  * trace, [n][trace_stride] entries) out.  Uploads descriptors, launches on
- * hip_stream and waits for that stream. */
+ * hip_stream and waits for that stream.  Its device workspace and pinned staging are this
+ * (device, stream)'s own (see Threads above). */
 int fmpnp_refine_batch(const fmpnp_problem *probs_host, int n, const fmpnp_options *opt, fmpnp_result *results,
                        fmpnp_trace_entry *trace, int trace_stride, void *hip_stream);
 
@@ -297,8 +303,10 @@ typedef struct {
  * [N][2], pts3d [N][3], K, R0, t0 (row-major) and results / trace ([max(n_levels, 1)][trace_stride]
  * entries, or NULL) are HOST memory.  opt->mode must be FMPNP_MODE_FORWARD; opt->dtype is the
  * packed storage.  Returns 0, FMPNP_ERANGE when an inlier maps outside the reference map (results
- * are still written), another FMPNP_E* code or a hipError_t.  The library keeps the device buffers
- * and a pinned staging buffer between calls (one call at a time per process). */
+ * are still written), another FMPNP_E* code or a hipError_t.  The library keeps, per (device,
+ * hip_stream), the device buffers, a pinned staging buffer and a second stream with two events
+ * between calls (see Threads above): with levels, the first level's channels are packed first and the
+ * other channels' pack and compute_cost run on that second stream under the first level's launch. */
 int fmpnp_feature_pnp(const void *query_chw, int dtype_query, int C, int H, int W, const void *ref_chw,
                       int dtype_ref, int C_ref, int H_ref, int W_ref, const double *ref_inliers,
                       const double *pts3d, int N, const double K[9], const double R0[9], const double t0[3],
