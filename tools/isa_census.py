@@ -31,7 +31,7 @@ SITES = {
 }
 
 
-def classify(op, args):
+def classify(op, args, spill_vgprs=frozenset()):
     if op.startswith(("v_fma_f64", "v_fmac_f64", "v_mul_f64", "v_add_f64", "v_max_f64", "v_min_f64",
                       "v_rcp_f64", "v_div_", "v_ldexp_f64", "v_frexp", "v_rndne_f64", "v_fract_f64",
                       "v_trunc_f64", "v_floor_f64", "v_sqrt_f64", "v_rsq_f64", "v_mul_f32", "v_fma_f32",
@@ -41,9 +41,12 @@ def classify(op, args):
     if op.startswith("v_cvt"):
         return "conversion"
     if op.startswith("v_readlane") or op.startswith("v_writelane"):
-        # to / from an SGPR: the SGPR spill slots live in VGPR lanes (v_writelane = spill, v_readlane =
-        # reload) -- the tail's rlane() reads are the exception (lm_decide: three values)
-        return "sgpr spill/reload (v_readlane/v_writelane)"
+        # to / from an SGPR: the SGPR spill slots live in VGPR lanes (v_writelane = spill, v_readlane from a
+        # spill VGPR = reload); other v_readlane are lane reads (the tail's rlane(), the LU fallback's rows)
+        vs = [a.strip() for a in args.split(",")]
+        if op.startswith("v_writelane") or (len(vs) > 1 and vs[1] in spill_vgprs):
+            return "sgpr spill/reload (v_readlane/v_writelane)"
+        return "cross-lane (dpp/permlane/readfirstlane)"
     if "_dpp" in op or op.startswith(("v_permlane", "ds_swizzle", "ds_bpermute", "v_readfirstlane")):
         return "cross-lane (dpp/permlane/readfirstlane)"
     if op.startswith(("v_mov", "v_cndmask")):
@@ -88,6 +91,8 @@ def census(asm_path):
         m = re.match(r"\s+\.(vgpr_count|sgpr_count|sgpr_spill_count|vgpr_spill_count|agpr_count):\s+(\d+)", l)
         if m:
             meta[m.group(1)] = int(m.group(2))
+    spill = frozenset(m.group(1) for l in lines[start:end]
+                      for m in [re.match(r"\s+v_writelane_b32 (v\d+),", l)] if m)
     segs = [("kernel entry", collections.Counter())]
     for l in lines[start:end]:
         s = l.strip()
@@ -99,7 +104,7 @@ def census(asm_path):
         if not s or s.startswith((";", ".")) or s.endswith(":"):
             continue
         parts = s.split(None, 1)
-        segs[-1][1][classify(parts[0], parts[1] if len(parts) > 1 else "")] += 1
+        segs[-1][1][classify(parts[0], parts[1] if len(parts) > 1 else "", spill)] += 1
     return meta, segs
 
 
